@@ -1,0 +1,202 @@
+"""Throughput benchmark of the MI355X MANO forward pass (driver contract).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--gather]
+
+One step = one forward (articulate -> blend GEMM -> skin) over B hands per GPU
+(BASELINE.json configs[1]: 65,536 hands, fp32 full pose, random betas), inputs
+resident in HBM before the timed region.  N > 1 runs one process per GPU
+(torch.distributed.run); shards are independent (no collective on the hot
+path), `--gather` adds the RCCL gather of verts + joints to GPU 0 (config C4).
+
+Rank 0 prints ONE JSON line with the whole-node hands/s, the roofline of the
+dominant kernel (per-kernel durations from HIP events recorded on the launch
+stream inside the timed steps) and, at N = 1, the CPU baseline: the float64
+per-hand restatement of mano_np.py (oracle/, "port") timed on this host.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "mano-hand_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+# Algorithmic work per hand (DESIGN.md "Rooflines").
+V, NCOL, K = 778, 2334, 145
+BLEND_FLOP_PER_HAND = 2 * NCOL * K                 # 676,860
+SKIN_BYTES_PER_HAND = NCOL * 4 * 2 + 16 * 12 * 4   # v_posed in + verts out + transforms = 19,440
+ARTICULATE_BYTES_PER_HAND = (10 + 48) * 4 + 16 * 12 * 4 + 16 * 3 * 4 + 152 * 4  # in + A + joints + X
+PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, spec
+PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=65536, help="hands per GPU per step")
+    ap.add_argument("--gather", action="store_true", help="RCCL gather of verts+joints to GPU 0")
+    ap.add_argument("--model", default=None, help="dump_model.py pickle (default: synthetic seed 0)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample length")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(params, seconds):
+    """float64 per-hand restatement (oracle.forward_one), one core, bounded sample."""
+    from oracle import mano_oracle
+    p = {k: (np.asarray(v, dtype=np.float64) if k not in ("parents", "faces") else v)
+         for k, v in params.items()}
+    rng = np.random.default_rng(1000)
+    betas = rng.normal(0, 1, (256, 10))
+    pose = rng.normal(0, 0.5, (256, 16, 3))
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        mano_oracle.forward_one(p, betas[n % 256], pose[n % 256])
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "hands/s", "cores": 1, "kind": "port",
+            "sample": f"{n} hands, one at a time, float64 numpy restatement of mano_np.py:81-115 "
+                      f"(oracle/mano_oracle.py forward_one), {dt:.1f} s on 1 host core"}
+
+
+def load_traffic(path, kernel, batch):
+    """HBM bytes per launch from a committed rocprofv3 --pmc summary, if it covers this batch."""
+    try:
+        with open(path) as f:
+            data = json.load(f)
+        ent = data["kernels"][kernel]
+        if int(data["batch"]) != batch:
+            return None
+        return float(ent["hbm_bytes_per_launch"])
+    except (OSError, KeyError, ValueError, TypeError):
+        return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from mano_amd import ManoHip, load_dump, synthetic_params
+    from mano_amd.distributed import gather_to_root
+    params = load_dump(args.model) if args.model else synthetic_params(0)
+    model = ManoHip(params, device=local)
+
+    B = args.batch
+    g = torch.Generator(device=dev).manual_seed(1001 + rank)
+    betas = torch.randn((B, 10), generator=g, device=dev)
+    pose = 0.5 * torch.randn((B, 16, 3), generator=g, device=dev)
+    verts = torch.empty((B, V, 3), device=dev)
+    joints = torch.empty((B, 16, 3), device=dev)
+    model.workspace(B)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(evs=None):
+        if evs is not None:
+            evs[0].record(stream)
+        model.stage_articulate(betas, pose, joints=joints)
+        if evs is not None:
+            evs[1].record(stream)
+        model.stage_blend(B)
+        if evs is not None:
+            evs[2].record(stream)
+        model.stage_skin(B, verts)
+        if evs is not None:
+            evs[3].record(stream)
+        if args.gather and world > 1:
+            gather_to_root(verts, B * world, root=0)
+            gather_to_root(joints, B * world, root=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(events[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    ms = {name: float(np.mean([e[a].elapsed_time(e[b]) for e in events]))
+          for name, a, b in (("articulate", 0, 1), ("blend", 1, 2), ("skin", 2, 3))}
+    kernels = {
+        "articulate": {"ms": ms["articulate"], "bound": "latency",
+                       "achieved_GBs": ARTICULATE_BYTES_PER_HAND * B / (ms["articulate"] * 1e-3) / 1e9},
+        "blend": {"ms": ms["blend"], "bound": "mfma",
+                  "achieved_TFLOPs": BLEND_FLOP_PER_HAND * B / (ms["blend"] * 1e-3) / 1e12},
+        "skin": {"ms": ms["skin"], "bound": "hbm",
+                 "achieved_GBs": SKIN_BYTES_PER_HAND * B / (ms["skin"] * 1e-3) / 1e9},
+    }
+    kernels["blend"]["frac"] = kernels["blend"]["achieved_TFLOPs"] / PEAK_FP32_TFLOPS
+    kernels["skin"]["frac"] = kernels["skin"]["achieved_GBs"] / PEAK_HBM_GBS
+    dominant = "blend" if ms["blend"] >= ms["skin"] else "skin"
+    if dominant == "blend":
+        ach = kernels["blend"]["achieved_TFLOPs"]
+        traffic = load_traffic(args.pmc, "blend", B)
+        roof = {"kernel": "blend_kernel", "bound": "mfma", "achieved": ach, "peak": PEAK_FP32_TFLOPS,
+                "unit": "TFLOP/s", "frac": ach / PEAK_FP32_TFLOPS, "traffic": traffic}
+    else:
+        ach = kernels["skin"]["achieved_GBs"]
+        traffic = load_traffic(args.pmc, "skin", B)
+        roof = {"kernel": "skin_kernel", "bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS,
+                "unit": "GB/s", "frac": ach / PEAK_HBM_GBS, "traffic": traffic}
+
+    if rank == 0:
+        total = B * world * args.steps
+        line = {
+            "metric": "posed hand meshes/sec (whole node)",
+            "value": total / dt,
+            "unit": "hands/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (random-init MANO arrays of the official shapes, seed 0; "
+                    "beta ~ N(0,1), pose ~ N(0,0.5^2) rad, generated on device)",
+            "config": {"workload": "C2: full-pose fp32 MANO forward, 65,536 hands per GPU"
+                       if B == 65536 else f"{B} hands per GPU",
+                       "hands_per_gpu": B, "global_batch": B * world, "outputs": "verts+joints",
+                       "gather_to_gpu0": bool(args.gather and world > 1),
+                       "parallelism": f"dp{world}"},
+            "roofline": roof,
+            "kernels": kernels,
+        }
+        if world == 1 and not args.no_cpu:
+            line["cpu_baseline"] = cpu_baseline(params, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    model.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

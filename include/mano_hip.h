@@ -1,0 +1,137 @@
+/*
+ * mano_hip.h -- C ABI of the MI355X (gfx950) MANO forward pass.
+ *
+ * The reference (reyuwei/MANO-Hand) has no FFI: its boundary is the Python
+ * object `MANOModel` in /root/reference/mano_np.py.  Each entry point below
+ * replaces a named piece of that object; the Python host layer
+ * (mano-hand_amd/mano_amd/) binds them with ctypes and re-creates the
+ * reference surface on top (see INTEGRATION.md for the binding stub).
+ *
+ * Conventions
+ *   - Every function returns an int status: MANO_OK (0) or a negative
+ *     MANO_E* code; mano_last_error() gives the message (thread-local).
+ *     No C++ exception crosses this ABI.
+ *   - Array arguments are plain pointers with the sizes stated.  Model arrays
+ *     given to mano_model_create are HOST float64 (the dump_model.py layout);
+ *     every pointer given to the forward / stage / helper calls is a DEVICE
+ *     pointer owned by the caller, on the model's device.
+ *   - Launches are asynchronous on `stream` (a hipStream_t; NULL = the
+ *     device's null stream).  Nothing blocks except model create/destroy.
+ *   - A model handle is bound to one device.  Calls on one handle may come
+ *     from several host threads only if they use distinct workspaces.
+ *   - Layouts are the reference's, row-major float32:
+ *       betas     [n][10]       (betas_stride = 10, or 0 for one shared vector)
+ *       pose      [n][16][3]    axis-angle per joint, joint 0 = global rotation
+ *       trans     [n][3]        (extension: the reference has no translation)
+ *       verts     [n][V][3]     = MANOModel.verts        (mano_np.py:113-115)
+ *       joints    [n][16][3]    posed joints = G[:, :3, 3] (mano_np.py:96-104)
+ *       rest_verts[n][V][3]     = MANOModel.rest_verts   (mano_np.py:91-93)
+ *       rest_joints[n][16][3]   = MANOModel.J            (mano_np.py:83)
+ *       rot_mats  [n][16][3][3] = MANOModel.R            (mano_np.py:86)
+ */
+#ifndef MANO_HIP_H
+#define MANO_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MANO_OK 0
+#define MANO_EINVAL (-1)   /* bad argument (null pointer, bad size, bad layout) */
+#define MANO_EHIP (-2)     /* HIP runtime error (allocation, copy, launch)      */
+#define MANO_ESMALL (-3)   /* workspace smaller than mano_workspace_bytes()     */
+#define MANO_ESTATE (-4)   /* handle destroyed / wrong device                   */
+
+#define MANO_N_JOINTS 16
+#define MANO_N_SHAPE 10
+#define MANO_N_POSE_FEATS 135
+#define MANO_N_PCA 45
+
+typedef struct mano_model mano_model; /* opaque, device-resident model buffer */
+
+/* Upload a model and build its device buffer.
+ * Replaces MANOModel.__init__'s array binding (mano_np.py:17-33) for the
+ * dump_model.py layout (dump_model.py:8-18).  Host float64 inputs:
+ *   mesh_template    [V][3]          mesh_shape_basis [V][3][10]
+ *   mesh_pose_basis  [V][3][135]     J_regressor      [16][V] (dense)
+ *   skinning_weights [V][16]         parents          [16] int32, -1 at root,
+ *                                                     parents[i] < i
+ *   pose_pca_basis   [45][45]        pose_pca_mean    [45]   (both nullable)
+ * The joint regression is folded in float64 here (J = Jreg.T + (Jreg.S) beta),
+ * then everything is stored as float32 in MFMA-ready layouts. */
+int mano_model_create(int device, int32_t n_verts,
+                      const double* mesh_template, const double* mesh_shape_basis,
+                      const double* mesh_pose_basis, const double* j_regressor,
+                      const double* skinning_weights, const int32_t* parents,
+                      const double* pose_pca_basis, const double* pose_pca_mean,
+                      mano_model** out);
+
+/* Free the device buffer.  NULL is accepted. */
+int mano_model_destroy(mano_model* model);
+
+/* Vertex count and device of a model. */
+int mano_model_info(const mano_model* model, int32_t* n_verts, int32_t* device);
+
+/* Device workspace (bytes) one forward over n_hands needs. */
+size_t mano_workspace_bytes(const mano_model* model, int64_t n_hands);
+
+/* Byte offsets of the intermediates inside the workspace (for inspection):
+ * pose-feature operand tiles, skinning transforms [n][16][3][4], v_posed. */
+int mano_workspace_offsets(const mano_model* model, int64_t n_hands,
+                           size_t* features_off, size_t* transforms_off,
+                           size_t* vposed_off);
+
+/* The full forward pass: MANOModel.update() (mano_np.py:79-115) for n_hands
+ * independent hands.  verts is required; joints, rest_verts, rest_joints,
+ * rot_mats and trans are nullable.  With rest_verts == NULL the v_posed
+ * intermediate lives in the workspace. */
+int mano_forward(const mano_model* model, int64_t n_hands,
+                 const float* betas, int64_t betas_stride, const float* pose,
+                 const float* trans, float* verts, float* joints,
+                 float* rest_verts, float* rest_joints, float* rot_mats,
+                 void* workspace, size_t workspace_bytes, void* stream);
+
+/* The three kernels of mano_forward, callable one at a time (same workspace
+ * carving), so each can be timed and checked alone.
+ *  articulate: Rodrigues (mano_np.py:117-148) + joint regression (:83) +
+ *              pose features (:87-91) + kinematic chain (:96-104) +
+ *              rest-pose removal (:106-110).
+ *  blend:      v_posed = T + S.beta + P.features (:81, :87-93) on MFMA.
+ *  skin:       LBS (:112-115), + trans. */
+int mano_stage_articulate(const mano_model* model, int64_t n_hands,
+                          const float* betas, int64_t betas_stride,
+                          const float* pose, const float* trans, float* joints,
+                          float* rest_joints, float* rot_mats, void* workspace,
+                          size_t workspace_bytes, void* stream);
+int mano_stage_blend(const mano_model* model, int64_t n_hands, float* rest_verts,
+                     void* workspace, size_t workspace_bytes, void* stream);
+int mano_stage_skin(const mano_model* model, int64_t n_hands,
+                    const float* rest_verts, const float* trans, float* verts,
+                    void* workspace, size_t workspace_bytes, void* stream);
+
+/* set_params' PCA branch (mano_np.py:66-72) on device:
+ *   pose[h] = [ rot[h] | pca[h][:n_comps] . pose_pca_basis[:n_comps] + mean ]
+ * pca [n][pca_stride] (stride 0 = shared), rot [n][3] (rot_stride 0 = shared). */
+int mano_pose_from_pca(const mano_model* model, int64_t n_hands, const float* pca,
+                       int32_t n_comps, int64_t pca_stride, const float* rot,
+                       int64_t rot_stride, float* pose, void* stream);
+
+/* MANOModel.rodrigues (mano_np.py:117-148): n axis-angle vectors [n][3] ->
+ * rotation matrices [n][3][3]. */
+int mano_rodrigues(int device, int64_t n, const float* axis_angle, float* rot,
+                   void* stream);
+
+/* Message of the last failed call on this thread ("" if none). */
+const char* mano_last_error(void);
+
+/* ABI version, bumped on any signature change. */
+int mano_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MANO_HIP_H */

@@ -1,0 +1,358 @@
+// mano_abi.hip -- the extern "C" boundary declared in include/mano_hip.h.
+//
+// Host side of the device-resident model buffer: validates arguments, folds the
+// joint regression in float64, packs the blend basis into MFMA B-fragment
+// tiles, carves the workspace and launches the kernels of mano_kernels.hip.
+// No C++ exception crosses the ABI; errors are status codes + a thread-local
+// message.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/mano_hip.h"
+#include "mano_internal.h"
+
+struct mano_model {
+  uint32_t magic;
+  int device;
+  mano::DeviceModel dm;
+  void* block;  // single device allocation holding every array of dm
+};
+
+namespace {
+
+constexpr uint32_t kMagic = 0x4d414e4fu;  // "MANO"
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(MANO_EHIP, "%s: %s (%d)", what, hipGetErrorString(e), int(e));
+}
+
+// Switch to the model's device for the duration of a call, restore after.
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  explicit DeviceGuard(int dev) {
+    err = hipGetDevice(&prev);
+    if (err == hipSuccess && prev != dev) err = hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int check_model(const mano_model* m) {
+  if (!m) return fail(MANO_EINVAL, "model handle is NULL");
+  if (m->magic != kMagic) return fail(MANO_ESTATE, "model handle is invalid or destroyed");
+  return MANO_OK;
+}
+
+int check_workspace(const mano_model* m, int64_t n, const void* ws, size_t ws_bytes) {
+  const mano::Workspace w = mano::workspace_layout(m->dm, n);
+  if (!ws) return fail(MANO_EINVAL, "workspace is NULL");
+  if (ws_bytes < w.total)
+    return fail(MANO_ESMALL, "workspace has %zu bytes, %zu needed for %lld hands", ws_bytes,
+                w.total, (long long)n);
+  if (reinterpret_cast<uintptr_t>(ws) % 256 != 0)
+    return fail(MANO_EINVAL, "workspace must be 256-byte aligned");
+  return MANO_OK;
+}
+
+constexpr int64_t kMaxHands = int64_t(1) << 30;
+
+}  // namespace
+
+extern "C" {
+
+int mano_abi_version(void) { return 1; }
+
+const char* mano_last_error(void) { return g_last_error.c_str(); }
+
+int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
+                      const double* mesh_shape_basis, const double* mesh_pose_basis,
+                      const double* j_regressor, const double* skinning_weights,
+                      const int32_t* parents, const double* pose_pca_basis,
+                      const double* pose_pca_mean, mano_model** out) {
+  using namespace mano;
+  g_last_error.clear();
+  if (!out) return fail(MANO_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (device < 0) return fail(MANO_EINVAL, "device %d is negative", device);
+  if (n_verts <= 0 || n_verts > (1 << 24)) return fail(MANO_EINVAL, "n_verts %d out of range", n_verts);
+  if (!mesh_template || !mesh_shape_basis || !mesh_pose_basis || !j_regressor ||
+      !skinning_weights || !parents)
+    return fail(MANO_EINVAL, "a required model array is NULL");
+  if ((pose_pca_basis == nullptr) != (pose_pca_mean == nullptr))
+    return fail(MANO_EINVAL, "pose_pca_basis and pose_pca_mean must both be given or both NULL");
+  if (parents[0] != -1) return fail(MANO_EINVAL, "parents[0] must be -1 (root)");
+  std::vector<int32_t> depth(kJoints, 0);
+  int max_depth = 0;
+  for (int i = 1; i < kJoints; ++i) {
+    if (parents[i] < 0 || parents[i] >= i)
+      return fail(MANO_EINVAL, "parents[%d] = %d must satisfy 0 <= p < %d", i, parents[i], i);
+    depth[i] = depth[parents[i]] + 1;
+    if (depth[i] > max_depth) max_depth = depth[i];
+  }
+
+  int n_dev = 0;
+  hipError_t e = hipGetDeviceCount(&n_dev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+  if (device >= n_dev) return fail(MANO_EINVAL, "device %d >= device count %d", device, n_dev);
+  DeviceGuard guard(device);
+  if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
+
+  const int V = n_verts;
+  const int n_cols = 3 * V;
+  const int n_col_tiles = (n_cols + kColTile - 1) / kColTile;
+
+  // ---- host float64 folds (J regression into beta space, mano_np.py:83) ----
+  std::vector<float> jt(kJoints * 3), js(kJoints * 3 * kShape);
+  for (int j = 0; j < kJoints; ++j) {
+    for (int c = 0; c < 3; ++c) {
+      double acc = 0.0;
+      for (int v = 0; v < V; ++v) acc += j_regressor[size_t(j) * V + v] * mesh_template[size_t(v) * 3 + c];
+      jt[j * 3 + c] = float(acc);
+      for (int s = 0; s < kShape; ++s) {
+        double a2 = 0.0;
+        for (int v = 0; v < V; ++v)
+          a2 += j_regressor[size_t(j) * V + v] * mesh_shape_basis[(size_t(v) * 3 + c) * kShape + s];
+        js[(j * 3 + c) * kShape + s] = float(a2);
+      }
+    }
+  }
+
+  // ---- blend basis as MFMA B-fragment tiles ----
+  // tile t, group g, lane l, slot q  <-  Basis[k = 2(4g+q) + (l>>5)][col = 32t + (l&31)]
+  std::vector<float> tiles(size_t(n_col_tiles) * kTileFloats, 0.f);
+  for (int t = 0; t < n_col_tiles; ++t)
+    for (int g = 0; g < kKGroups; ++g)
+      for (int l = 0; l < 64; ++l)
+        for (int q = 0; q < 4; ++q) {
+          const int k = 2 * (4 * g + q) + (l >> 5);
+          const int col = t * kColTile + (l & 31);
+          float v = 0.f;
+          if (k < kK && col < n_cols) {
+            if (k < kShape)
+              v = float(mesh_shape_basis[size_t(col) * kShape + k]);
+            else
+              v = float(mesh_pose_basis[size_t(col) * kPoseFeats + (k - kShape)]);
+          }
+          tiles[((size_t(t) * kKGroups + g) * 64 + l) * 4 + q] = v;
+        }
+  std::vector<float> tmpl(size_t(n_col_tiles) * kColTile, 0.f);
+  for (int i = 0; i < n_cols; ++i) tmpl[i] = float(mesh_template[i]);
+  std::vector<float> wts(size_t(V) * kJoints);
+  for (size_t i = 0; i < wts.size(); ++i) wts[i] = float(skinning_weights[i]);
+  std::vector<float> pca(kPca * kPca, 0.f), pmean(kPca, 0.f);
+  if (pose_pca_basis) {
+    for (int i = 0; i < kPca * kPca; ++i) pca[i] = float(pose_pca_basis[i]);
+    for (int i = 0; i < kPca; ++i) pmean[i] = float(pose_pca_mean[i]);
+  }
+
+  // ---- one device block, 256-B aligned sub-arrays ----
+  struct Part { const void* src; size_t bytes; size_t off; };
+  std::vector<Part> parts = {
+      {tiles.data(), tiles.size() * 4, 0}, {tmpl.data(), tmpl.size() * 4, 0},
+      {wts.data(), wts.size() * 4, 0},     {jt.data(), jt.size() * 4, 0},
+      {js.data(), js.size() * 4, 0},       {parents, kJoints * 4, 0},
+      {depth.data(), kJoints * 4, 0},      {pca.data(), pca.size() * 4, 0},
+      {pmean.data(), pmean.size() * 4, 0}};
+  size_t total = 0;
+  for (auto& p : parts) {
+    p.off = total;
+    total = align256(total + p.bytes);
+  }
+  void* block = nullptr;
+  e = hipMalloc(&block, total);
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc(model buffer)");
+  for (auto& p : parts) {
+    e = hipMemcpy(static_cast<char*>(block) + p.off, p.src, p.bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      (void)hipFree(block);
+      return hip_fail(e, "hipMemcpy(model buffer)");
+    }
+  }
+  mano_model* m = new (std::nothrow) mano_model();
+  if (!m) {
+    (void)hipFree(block);
+    return fail(MANO_EINVAL, "out of host memory");
+  }
+  char* b = static_cast<char*>(block);
+  m->magic = kMagic;
+  m->device = device;
+  m->block = block;
+  m->dm.basis_tiles = reinterpret_cast<float*>(b + parts[0].off);
+  m->dm.template_cols = reinterpret_cast<float*>(b + parts[1].off);
+  m->dm.weights = reinterpret_cast<float*>(b + parts[2].off);
+  m->dm.joint_template = reinterpret_cast<float*>(b + parts[3].off);
+  m->dm.joint_shape = reinterpret_cast<float*>(b + parts[4].off);
+  m->dm.parents = reinterpret_cast<int32_t*>(b + parts[5].off);
+  m->dm.depth = reinterpret_cast<int32_t*>(b + parts[6].off);
+  m->dm.pca_basis = reinterpret_cast<float*>(b + parts[7].off);
+  m->dm.pca_mean = reinterpret_cast<float*>(b + parts[8].off);
+  m->dm.max_depth = max_depth;
+  m->dm.n_verts = V;
+  m->dm.n_cols = n_cols;
+  m->dm.n_col_tiles = n_col_tiles;
+  *out = m;
+  return MANO_OK;
+}
+
+int mano_model_destroy(mano_model* m) {
+  g_last_error.clear();
+  if (!m) return MANO_OK;
+  if (m->magic != kMagic) return fail(MANO_ESTATE, "model handle is invalid or destroyed");
+  DeviceGuard guard(m->device);
+  m->magic = 0;
+  hipError_t e = hipFree(m->block);
+  delete m;
+  if (e != hipSuccess) return hip_fail(e, "hipFree(model buffer)");
+  return MANO_OK;
+}
+
+int mano_model_info(const mano_model* m, int32_t* n_verts, int32_t* device) {
+  if (int rc = check_model(m)) return rc;
+  if (n_verts) *n_verts = m->dm.n_verts;
+  if (device) *device = m->device;
+  return MANO_OK;
+}
+
+size_t mano_workspace_bytes(const mano_model* m, int64_t n) {
+  if (check_model(m) || n < 0) return 0;
+  return mano::workspace_layout(m->dm, n).total;
+}
+
+int mano_workspace_offsets(const mano_model* m, int64_t n, size_t* features_off,
+                           size_t* transforms_off, size_t* vposed_off) {
+  if (int rc = check_model(m)) return rc;
+  if (n < 0) return fail(MANO_EINVAL, "n_hands %lld < 0", (long long)n);
+  const mano::Workspace w = mano::workspace_layout(m->dm, n);
+  if (features_off) *features_off = w.features_off;
+  if (transforms_off) *transforms_off = w.transforms_off;
+  if (vposed_off) *vposed_off = w.vposed_off;
+  return MANO_OK;
+}
+
+int mano_stage_articulate(const mano_model* m, int64_t n, const float* betas,
+                          int64_t betas_stride, const float* pose, const float* trans,
+                          float* joints, float* rest_joints, float* rot_mats, void* ws,
+                          size_t ws_bytes, void* stream) {
+  if (int rc = check_model(m)) return rc;
+  if (n < 0 || n > kMaxHands) return fail(MANO_EINVAL, "n_hands %lld out of range", (long long)n);
+  if (n == 0) return MANO_OK;
+  if (!betas || !pose) return fail(MANO_EINVAL, "betas and pose are required");
+  if (betas_stride != 0 && betas_stride < mano::kShape)
+    return fail(MANO_EINVAL, "betas_stride %lld must be 0 or >= 10", (long long)betas_stride);
+  if (int rc = check_workspace(m, n, ws, ws_bytes)) return rc;
+  DeviceGuard guard(m->device);
+  if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
+  const mano::Workspace w = mano::workspace_layout(m->dm, n);
+  char* base = static_cast<char*>(ws);
+  hipError_t e = mano::launch_articulate(
+      m->dm, n, betas, betas_stride, pose, trans, reinterpret_cast<float*>(base + w.features_off),
+      reinterpret_cast<float*>(base + w.transforms_off), joints, rest_joints, rot_mats,
+      static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "articulate launch");
+  return MANO_OK;
+}
+
+int mano_stage_blend(const mano_model* m, int64_t n, float* rest_verts, void* ws, size_t ws_bytes,
+                     void* stream) {
+  if (int rc = check_model(m)) return rc;
+  if (n < 0 || n > kMaxHands) return fail(MANO_EINVAL, "n_hands %lld out of range", (long long)n);
+  if (n == 0) return MANO_OK;
+  if (int rc = check_workspace(m, n, ws, ws_bytes)) return rc;
+  DeviceGuard guard(m->device);
+  if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
+  const mano::Workspace w = mano::workspace_layout(m->dm, n);
+  char* base = static_cast<char*>(ws);
+  float* vp = rest_verts ? rest_verts : reinterpret_cast<float*>(base + w.vposed_off);
+  hipError_t e = mano::launch_blend(m->dm, n, reinterpret_cast<const float*>(base + w.features_off),
+                                    vp, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "blend launch");
+  return MANO_OK;
+}
+
+int mano_stage_skin(const mano_model* m, int64_t n, const float* rest_verts, const float* trans,
+                    float* verts, void* ws, size_t ws_bytes, void* stream) {
+  if (int rc = check_model(m)) return rc;
+  if (n < 0 || n > kMaxHands) return fail(MANO_EINVAL, "n_hands %lld out of range", (long long)n);
+  if (n == 0) return MANO_OK;
+  if (!verts) return fail(MANO_EINVAL, "verts is required");
+  if (int rc = check_workspace(m, n, ws, ws_bytes)) return rc;
+  DeviceGuard guard(m->device);
+  if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
+  const mano::Workspace w = mano::workspace_layout(m->dm, n);
+  char* base = static_cast<char*>(ws);
+  const float* vp = rest_verts ? rest_verts : reinterpret_cast<const float*>(base + w.vposed_off);
+  hipError_t e =
+      mano::launch_skin(m->dm, n, reinterpret_cast<const float*>(base + w.transforms_off), vp,
+                        trans, verts, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "skin launch");
+  return MANO_OK;
+}
+
+int mano_forward(const mano_model* m, int64_t n, const float* betas, int64_t betas_stride,
+                 const float* pose, const float* trans, float* verts, float* joints,
+                 float* rest_verts, float* rest_joints, float* rot_mats, void* ws,
+                 size_t ws_bytes, void* stream) {
+  g_last_error.clear();
+  if (int rc = check_model(m)) return rc;
+  if (n > 0 && !verts) return fail(MANO_EINVAL, "verts is required");
+  if (int rc = mano_stage_articulate(m, n, betas, betas_stride, pose, trans, joints, rest_joints,
+                                     rot_mats, ws, ws_bytes, stream))
+    return rc;
+  if (int rc = mano_stage_blend(m, n, rest_verts, ws, ws_bytes, stream)) return rc;
+  return mano_stage_skin(m, n, rest_verts, trans, verts, ws, ws_bytes, stream);
+}
+
+int mano_pose_from_pca(const mano_model* m, int64_t n, const float* pca, int32_t n_comps,
+                       int64_t pca_stride, const float* rot, int64_t rot_stride, float* pose,
+                       void* stream) {
+  if (int rc = check_model(m)) return rc;
+  if (n < 0 || n > kMaxHands) return fail(MANO_EINVAL, "n_hands %lld out of range", (long long)n);
+  if (n_comps < 0 || n_comps > mano::kPca)
+    return fail(MANO_EINVAL, "n_comps %d must be in [0, 45] (mano_np.py:55-56)", n_comps);
+  if (pca_stride != 0 && pca_stride < n_comps)
+    return fail(MANO_EINVAL, "pca_stride %lld < n_comps %d", (long long)pca_stride, n_comps);
+  if (rot_stride != 0 && rot_stride < 3)
+    return fail(MANO_EINVAL, "rot_stride %lld must be 0 or >= 3", (long long)rot_stride);
+  if (n == 0) return MANO_OK;
+  if (!pose || (n_comps > 0 && !pca)) return fail(MANO_EINVAL, "pose / pca pointer is NULL");
+  DeviceGuard guard(m->device);
+  if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
+  hipError_t e = mano::launch_pose_from_pca(m->dm, n, pca, n_comps, pca_stride, rot, rot_stride,
+                                            pose, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "pose_from_pca launch");
+  return MANO_OK;
+}
+
+int mano_rodrigues(int device, int64_t n, const float* aa, float* rot, void* stream) {
+  if (n < 0 || n > kMaxHands * 16) return fail(MANO_EINVAL, "n %lld out of range", (long long)n);
+  if (n == 0) return MANO_OK;
+  if (!aa || !rot) return fail(MANO_EINVAL, "axis_angle / rot pointer is NULL");
+  if (device < 0) return fail(MANO_EINVAL, "device %d is negative", device);
+  DeviceGuard guard(device);
+  if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
+  hipError_t e = mano::launch_rodrigues(n, aa, rot, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "rodrigues launch");
+  return MANO_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,76 @@
+// mano_internal.h -- device-buffer layout shared by the C-ABI host code
+// (mano_abi.hip) and the gfx950 kernels (mano_kernels.hip).  Not installed.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace mano {
+
+constexpr int kJoints = 16;                    // mano_np.py:35
+constexpr int kShape = 10;                     // mano_np.py:36
+constexpr int kPoseFeats = 9 * (kJoints - 1);  // 135, mano_np.py:87-91
+constexpr int kPca = 45;                       // dump_model.py:8
+
+// Blend GEMM operand geometry (v_mfma_f32_32x32x2_f32: one K-pair per step).
+// Row k of the combined basis: k < 10 shape direction k, 10 <= k < 145 pose
+// direction k - 10, k = 145 zero pad.
+constexpr int kK = kShape + kPoseFeats;        // 145
+constexpr int kKSteps = (kK + 1) / 2;          // 73 MFMA steps (K padded to 146)
+constexpr int kKGroups = (kKSteps + 3) / 4;    // 19 float4 groups per lane
+constexpr int kTileFloats = kKGroups * 64 * 4; // 4864 floats = 19,456 B per tile
+constexpr int kHandTile = 32;                  // hands per MFMA row tile
+constexpr int kColTile = 32;                   // basis columns per MFMA col tile
+constexpr int kTransformFloats = kJoints * 12; // 3x4 skinning transform per joint
+
+// Device-resident model buffer (float32, layouts chosen for the kernels).
+struct DeviceModel {
+  float* basis_tiles;   // [n_col_tiles][kKGroups][64][4] MFMA B fragments
+  float* template_cols; // [n_col_tiles * 32] mesh_template flattened, zero-padded
+  float* weights;       // [V][16] skinning weights
+  float* joint_template;// [16][3]   J_regressor . mesh_template       (float64 fold)
+  float* joint_shape;   // [16][3][10] J_regressor . mesh_shape_basis (float64 fold)
+  int32_t* parents;     // [16], -1 at the root
+  int32_t* depth;       // [16] depth in the kinematic tree (root 0)
+  float* pca_basis;     // [45][45]
+  float* pca_mean;      // [45]
+  int32_t max_depth;
+  int32_t n_verts;
+  int32_t n_cols;       // 3V
+  int32_t n_col_tiles;  // ceil(3V / 32)
+};
+
+// Workspace carving (all offsets 256-B aligned).
+struct Workspace {
+  size_t features_off, transforms_off, vposed_off, total;
+};
+
+inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+inline Workspace workspace_layout(const DeviceModel& m, int64_t n) {
+  Workspace w;
+  const int64_t n_tiles = (n + kHandTile - 1) / kHandTile;
+  w.features_off = 0;
+  w.transforms_off = align256(w.features_off + size_t(n_tiles) * kTileFloats * sizeof(float));
+  w.vposed_off = align256(w.transforms_off + size_t(n) * kTransformFloats * sizeof(float));
+  w.total = align256(w.vposed_off + size_t(n) * m.n_cols * sizeof(float));
+  return w;
+}
+
+// Kernel launchers (mano_kernels.hip).  All asynchronous on `stream`.
+hipError_t launch_articulate(const DeviceModel& m, int64_t n, const float* betas,
+                             int64_t betas_stride, const float* pose, const float* trans,
+                             float* features, float* transforms, float* joints,
+                             float* rest_joints, float* rot_mats, hipStream_t stream);
+hipError_t launch_blend(const DeviceModel& m, int64_t n, const float* features,
+                        float* vposed, hipStream_t stream);
+hipError_t launch_skin(const DeviceModel& m, int64_t n, const float* transforms,
+                       const float* vposed, const float* trans, float* verts,
+                       hipStream_t stream);
+hipError_t launch_pose_from_pca(const DeviceModel& m, int64_t n, const float* pca,
+                                int n_comps, int64_t pca_stride, const float* rot,
+                                int64_t rot_stride, float* pose, hipStream_t stream);
+hipError_t launch_rodrigues(int64_t n, const float* aa, float* rot, hipStream_t stream);
+
+}  // namespace mano

@@ -1,0 +1,101 @@
+"""ctypes binding of `include/mano_hip.h` (the C-ABI of libmano_hip.so).
+
+Loads the in-tree gfx950 library; there is no fallback: if the library is
+missing or fails to load, `lib()` raises `MissingExtensionError` so a product
+call can never silently run anything else.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmano_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "mano_hip.h")
+
+MANO_OK, MANO_EINVAL, MANO_EHIP, MANO_ESMALL, MANO_ESTATE = 0, -1, -2, -3, -4
+_CODE_NAMES = {MANO_EINVAL: "MANO_EINVAL", MANO_EHIP: "MANO_EHIP",
+               MANO_ESMALL: "MANO_ESMALL", MANO_ESTATE: "MANO_ESTATE"}
+
+
+class MissingExtensionError(RuntimeError):
+    """libmano_hip.so is not built / not loadable: the HIP path cannot run."""
+
+
+class ManoError(RuntimeError):
+    def __init__(self, code, message):
+        super().__init__(f"{_CODE_NAMES.get(code, code)}: {message}")
+        self.code = code
+
+
+_p = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int32
+_dptr = ctypes.POINTER(ctypes.c_double)
+_ipt = ctypes.POINTER(ctypes.c_int32)
+
+# name -> (restype, argtypes); mirrors include/mano_hip.h one to one.
+SIGNATURES = {
+    "mano_abi_version": (ctypes.c_int, []),
+    "mano_last_error": (ctypes.c_char_p, []),
+    "mano_model_create": (ctypes.c_int, [ctypes.c_int, _i32, _dptr, _dptr, _dptr, _dptr, _dptr,
+                                         _ipt, _dptr, _dptr, ctypes.POINTER(_p)]),
+    "mano_model_destroy": (ctypes.c_int, [_p]),
+    "mano_model_info": (ctypes.c_int, [_p, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
+    "mano_workspace_bytes": (ctypes.c_size_t, [_p, _i64]),
+    "mano_workspace_offsets": (ctypes.c_int, [_p, _i64, ctypes.POINTER(ctypes.c_size_t),
+                                              ctypes.POINTER(ctypes.c_size_t),
+                                              ctypes.POINTER(ctypes.c_size_t)]),
+    "mano_forward": (ctypes.c_int, [_p, _i64, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p,
+                                    ctypes.c_size_t, _p]),
+    "mano_stage_articulate": (ctypes.c_int, [_p, _i64, _p, _i64, _p, _p, _p, _p, _p, _p,
+                                             ctypes.c_size_t, _p]),
+    "mano_stage_blend": (ctypes.c_int, [_p, _i64, _p, _p, ctypes.c_size_t, _p]),
+    "mano_stage_skin": (ctypes.c_int, [_p, _i64, _p, _p, _p, _p, ctypes.c_size_t, _p]),
+    "mano_pose_from_pca": (ctypes.c_int, [_p, _i64, _p, _i32, _i64, _p, _i64, _p, _p]),
+    "mano_rodrigues": (ctypes.c_int, [ctypes.c_int, _i64, _p, _p, _p]),
+}
+
+_LIB = None
+
+
+def header_functions(path: str = HEADER_PATH):
+    """Names of every function the public header declares."""
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(mano_[a-z_]+)\s*\(", text)))
+
+
+def lib() -> ctypes.CDLL:
+    """Load libmano_hip.so once (RTLD_GLOBAL off) and declare every signature."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise MissingExtensionError(
+            f"{LIB_PATH} is not built; run `make -C mano-hand_amd` or "
+            "`python -c 'import __graft_entry__ as g; g.build()'`")
+    try:
+        # torch (if imported) already holds libamdhip64.so.7; the same SONAME
+        # resolves to that copy, so torch and this library share one HIP runtime.
+        handle = ctypes.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover - depends on the box
+        raise MissingExtensionError(f"cannot load {LIB_PATH}: {e}") from e
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(handle, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = handle
+    return _LIB
+
+
+def check(rc: int) -> None:
+    if rc != MANO_OK:
+        msg = lib().mano_last_error()
+        raise ManoError(rc, msg.decode() if msg else "")
+
+
+def last_error() -> str:
+    msg = lib().mano_last_error()
+    return msg.decode() if msg else ""

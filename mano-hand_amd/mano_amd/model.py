@@ -1,0 +1,369 @@
+"""Host layer over the gfx950 C-ABI: the batched engine and the drop-in MANOModel.
+
+`ManoHip`   -- device-resident model + batched forward over torch device
+               tensors (betas (B,10), pose (B,16,3), trans (B,3) -> verts,
+               joints, ...).  Every computation is a launch of libmano_hip.so;
+               torch only supplies device memory and the stream.
+`MANOModel` -- the reference's object API (/root/reference/mano_np.py:5-201):
+               same constructor argument, `set_params` / `update` semantics and
+               quirks, attributes `verts J R rest_verts pose shape rot faces
+               parents`, `rodrigues`, `with_zeros`, `pack`, `export_obj`.
+               Outputs are float64 numpy copies as in the reference; the
+               forward itself runs on the GPU (float32).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from . import _abi
+from .model_io import (MODEL_KEYS, N_JOINTS, N_SHAPE, check_layout, load_dump,
+                       parents_to_int)
+
+_F64P = ctypes.POINTER(ctypes.c_double)
+
+
+def _dptr(a: np.ndarray):
+    return a.ctypes.data_as(_F64P)
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream_handle(device: torch.device, stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class ManoHip:
+    """Device-resident MANO model on one GPU (wraps a `mano_model*` handle)."""
+
+    def __init__(self, params: Dict[str, object], device=None):
+        check_layout(params)
+        if device is None:
+            idx = torch.cuda.current_device()
+        elif isinstance(device, int):
+            idx = device
+        else:
+            d = torch.device(device)
+            idx = d.index if d.index is not None else torch.cuda.current_device()
+        self.device = torch.device("cuda", idx)
+        lib = _abi.lib()
+        f64 = lambda k: np.ascontiguousarray(np.asarray(params[k], dtype=np.float64))  # noqa: E731
+        tmpl = f64("mesh_template")
+        self.n_verts = int(tmpl.shape[0])
+        sdirs, pdirs = f64("mesh_shape_basis"), f64("mesh_pose_basis")
+        if sdirs.shape[2] != N_SHAPE:
+            raise ValueError(f"mesh_shape_basis must have {N_SHAPE} shape directions, got {sdirs.shape}")
+        if len(params["parents"]) != N_JOINTS:
+            raise ValueError(f"the HIP kernels are built for {N_JOINTS} joints")
+        jreg, wts = f64("J_regressor"), f64("skinning_weights")
+        par = parents_to_int(params["parents"])
+        pca = params.get("pose_pca_basis")
+        mean = params.get("pose_pca_mean")
+        pca = None if pca is None else np.ascontiguousarray(np.asarray(pca, dtype=np.float64))
+        mean = None if mean is None else np.ascontiguousarray(np.asarray(mean, dtype=np.float64))
+        if pca is not None and (pca.shape != (45, 45) or mean.shape != (45,)):
+            raise ValueError(f"pose_pca_basis/mean must be (45,45)/(45,), got {pca.shape}/{mean.shape}")
+        torch.cuda.init()
+        handle = ctypes.c_void_p()
+        _abi.check(lib.mano_model_create(
+            self.device.index, self.n_verts, _dptr(tmpl), _dptr(sdirs), _dptr(pdirs), _dptr(jreg),
+            _dptr(wts), par.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+            None if pca is None else _dptr(pca), None if mean is None else _dptr(mean),
+            ctypes.byref(handle)))
+        self._h = handle
+        self._ws = None
+        self._ws_hands = -1
+
+    # ------------------------------------------------------------------ utils
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _abi.check(_abi.lib().mano_model_destroy(self._h))
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - interpreter teardown order varies
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def workspace_bytes(self, n: int) -> int:
+        return int(_abi.lib().mano_workspace_bytes(self._h, n))
+
+    def workspace_offsets(self, n: int):
+        a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        _abi.check(_abi.lib().mano_workspace_offsets(self._h, n, ctypes.byref(a), ctypes.byref(b),
+                                                     ctypes.byref(c)))
+        return a.value, b.value, c.value
+
+    def workspace(self, n: int) -> torch.Tensor:
+        """Cached device workspace large enough for `n` hands."""
+        if self._ws is None or self._ws_hands < n:
+            nbytes = max(self.workspace_bytes(n), 256)
+            self._ws = torch.empty(nbytes + 256, dtype=torch.uint8, device=self.device)
+            self._ws_hands = n
+        return self._ws
+
+    def _ws_args(self, n):
+        ws = self.workspace(n)
+        base = ws.data_ptr()
+        aligned = (base + 255) & ~255
+        return ctypes.c_void_p(aligned), ctypes.c_size_t(ws.numel() - (aligned - base))
+
+    def _check(self, t: Optional[torch.Tensor], name: str, shape) -> Optional[torch.Tensor]:
+        if t is None:
+            return None
+        if not isinstance(t, torch.Tensor):
+            raise TypeError(f"{name} must be a torch tensor on {self.device}")
+        if t.device != self.device or t.dtype != torch.float32:
+            raise ValueError(f"{name} must be float32 on {self.device}, got {t.dtype} on {t.device}")
+        if tuple(t.shape) != tuple(shape):
+            raise ValueError(f"{name} has shape {tuple(t.shape)}, expected {tuple(shape)}")
+        if not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+        return t
+
+    def _inputs(self, betas, pose, trans):
+        if not isinstance(pose, torch.Tensor):
+            raise TypeError("pose must be a torch tensor")
+        B = pose.shape[0]
+        pose = self._check(pose.reshape(B, N_JOINTS, 3) if pose.dim() == 2 else pose, "pose",
+                           (B, N_JOINTS, 3))
+        if betas.dim() == 1:
+            betas = self._check(betas, "betas", (N_SHAPE,))
+            bstride = 0
+        else:
+            betas = self._check(betas, "betas", (B, N_SHAPE))
+            bstride = N_SHAPE
+        trans = self._check(trans, "trans", (B, 3))
+        return B, betas, bstride, pose, trans
+
+    # --------------------------------------------------------------- forward
+    def forward(self, betas: torch.Tensor, pose: torch.Tensor, trans: Optional[torch.Tensor] = None,
+                *, joints: bool = True, rest_verts: bool = False, rest_joints: bool = False,
+                rot_mats: bool = False, out: Optional[Dict[str, torch.Tensor]] = None,
+                stream=None) -> Dict[str, torch.Tensor]:
+        """Batched MANOModel.update() (mano_np.py:79-115) on the GPU.
+
+        betas (B,10) or (10,) shared, pose (B,16,3) or (B,48) axis-angle,
+        trans (B,3) optional.  Returns float32 device tensors: verts (B,V,3),
+        and on request joints (B,16,3) posed, rest_verts (B,V,3),
+        rest_joints (B,16,3), rot_mats (B,16,3,3).
+        """
+        B, betas, bstride, pose, trans = self._inputs(betas, pose, trans)
+        V = self.n_verts
+        res = dict(out) if out else {}
+
+        def buf(name, shape, want):
+            if not want:
+                return None
+            t = res.get(name)
+            if t is None:
+                t = torch.empty(shape, dtype=torch.float32, device=self.device)
+                res[name] = t
+            return self._check(t, name, shape)
+
+        v = buf("verts", (B, V, 3), True)
+        j = buf("joints", (B, N_JOINTS, 3), joints)
+        rv = buf("rest_verts", (B, V, 3), rest_verts)
+        rj = buf("rest_joints", (B, N_JOINTS, 3), rest_joints)
+        rm = buf("rot_mats", (B, N_JOINTS, 3, 3), rot_mats)
+        ws, wsb = self._ws_args(B)
+        _abi.check(_abi.lib().mano_forward(
+            self._h, B, _ptr(betas), bstride, _ptr(pose), _ptr(trans), _ptr(v), _ptr(j), _ptr(rv),
+            _ptr(rj), _ptr(rm), ws, wsb, _stream_handle(self.device, stream)))
+        return res
+
+    # ---- the three kernels one at a time (per-kernel timing / unit checks) ----
+    def stage_articulate(self, betas, pose, trans=None, joints=None, rest_joints=None,
+                         rot_mats=None, stream=None):
+        B, betas, bstride, pose, trans = self._inputs(betas, pose, trans)
+        ws, wsb = self._ws_args(B)
+        _abi.check(_abi.lib().mano_stage_articulate(
+            self._h, B, _ptr(betas), bstride, _ptr(pose), _ptr(trans), _ptr(joints),
+            _ptr(rest_joints), _ptr(rot_mats), ws, wsb, _stream_handle(self.device, stream)))
+
+    def stage_blend(self, n: int, rest_verts=None, stream=None):
+        ws, wsb = self._ws_args(n)
+        _abi.check(_abi.lib().mano_stage_blend(self._h, n, _ptr(rest_verts), ws, wsb,
+                                               _stream_handle(self.device, stream)))
+
+    def stage_skin(self, n: int, verts: torch.Tensor, rest_verts=None, trans=None, stream=None):
+        ws, wsb = self._ws_args(n)
+        _abi.check(_abi.lib().mano_stage_skin(self._h, n, _ptr(rest_verts), _ptr(trans),
+                                              _ptr(verts), ws, wsb,
+                                              _stream_handle(self.device, stream)))
+
+    def intermediates(self, n: int) -> Dict[str, torch.Tensor]:
+        """Views of the workspace after a stage/forward call over `n` hands:
+        `features` (ceil(n/32), 19, 64, 4) MFMA A tiles, `transforms`
+        (n,16,3,4) skinning transforms, `vposed` (n,V,3)."""
+        ws = self.workspace(n)
+        base = ws.data_ptr()
+        shift = ((base + 255) & ~255) - base
+        fo, to, vo = self.workspace_offsets(n)
+        f32 = ws[shift:shift + (ws.numel() - shift) // 4 * 4].view(torch.float32)
+        nt = (n + 31) // 32
+        return {
+            "features": f32[fo // 4: fo // 4 + nt * 4864].view(nt, 19, 64, 4),
+            "transforms": f32[to // 4: to // 4 + n * 192].view(n, N_JOINTS, 3, 4),
+            "vposed": f32[vo // 4: vo // 4 + n * self.n_verts * 3].view(n, self.n_verts, 3),
+        }
+
+    # ---- set_params' PCA branch and the Rodrigues helper on device ----
+    def pose_from_pca(self, pca: torch.Tensor, rot: Optional[torch.Tensor] = None,
+                      stream=None) -> torch.Tensor:
+        """pose (B,16,3) = [rot | pca @ pose_pca_basis[:N] + mean] (mano_np.py:66-72)."""
+        if pca.dim() == 1:
+            pca = pca[None]
+        B, N = pca.shape
+        self._check(pca, "pose_pca", (B, N))
+        if rot is not None:
+            rot = self._check(rot.reshape(-1, 3), "global_rot", (rot.numel() // 3, 3))
+            rot_stride = 0 if rot.shape[0] == 1 else 3
+            if rot.shape[0] not in (1, B):
+                raise ValueError("global_rot must have 1 or B rows")
+        else:
+            rot_stride = 0
+        pose = torch.empty((B, N_JOINTS, 3), dtype=torch.float32, device=self.device)
+        _abi.check(_abi.lib().mano_pose_from_pca(self._h, B, _ptr(pca), N, N, _ptr(rot), rot_stride,
+                                                 _ptr(pose), _stream_handle(self.device, stream)))
+        return pose
+
+    def rodrigues(self, axis_angle: torch.Tensor, stream=None) -> torch.Tensor:
+        """(..., 3) axis-angle -> (..., 3, 3) rotations (mano_np.py:117-148)."""
+        aa = axis_angle.reshape(-1, 3).contiguous()
+        self._check(aa, "axis_angle", (aa.shape[0], 3))
+        rot = torch.empty((aa.shape[0], 3, 3), dtype=torch.float32, device=self.device)
+        _abi.check(_abi.lib().mano_rodrigues(self.device.index, aa.shape[0], _ptr(aa), _ptr(rot),
+                                             _stream_handle(self.device, stream)))
+        return rot.reshape(axis_angle.shape[:-1] + (3, 3))
+
+
+class MANOModel:
+    """Drop-in for the reference `MANOModel` (mano_np.py:5-201), GPU-backed.
+
+    * Call `set_params` to set pose and shape params.
+    * Call `export_obj` to export to obj file.
+    """
+
+    def __init__(self, model_path, device=None):
+        """model_path: a model dumped by `dump_model.py` (mano_np.py:11-46)."""
+        params = load_dump(model_path)
+        self._init_from_params(params, device)
+
+    @classmethod
+    def from_params(cls, params: Dict[str, object], device=None) -> "MANOModel":
+        self = cls.__new__(cls)
+        self._init_from_params(params, device)
+        return self
+
+    def _init_from_params(self, params, device):
+        self.pose_pca_basis = params["pose_pca_basis"]
+        self.pose_pca_mean = params["pose_pca_mean"]
+        self.J_regressor = params["J_regressor"]
+        self.skinning_weights = params["skinning_weights"]
+        self.mesh_pose_basis = params["mesh_pose_basis"]
+        self.mesh_shape_basis = params["mesh_shape_basis"]
+        self.mesh_template = params["mesh_template"]
+        self.faces = params["faces"]
+        self.parents = params["parents"]
+        self.n_joints = 16
+        self.n_shape_params = 10
+        self.engine = ManoHip({k: params[k] for k in MODEL_KEYS}, device=device)
+        self.device = self.engine.device
+        self.pose = np.zeros((self.n_joints, 3))
+        self.shape = np.zeros(self.n_shape_params)
+        self.rot = np.zeros([1, 3])
+        self.trans = np.zeros(3)
+        self.verts = None
+        self.rest_verts = None
+        self.J = None
+        self.R = None
+        self.joints = None
+        self.update()
+
+    def _dev(self, a) -> torch.Tensor:
+        return torch.as_tensor(np.asarray(a, dtype=np.float32)).to(self.device)
+
+    def set_params(self, pose_abs=None, pose_pca=None, shape=None, global_rot=None, trans=None):
+        """Same semantics as mano_np.py:48-77, plus an optional translation.
+
+        pose_abs: per-joint axis-angle, shape [16, 3] (or [48]); taken verbatim.
+        pose_pca: [N] PCA coefficients, 0 < N <= 45; pose = c.basis[:N] + mean
+          with the stored global rotation `rot` prepended.
+        global_rot: only read on the pose_pca branch, then kept in `rot`.
+        shape: the 10 shape coefficients.
+        trans: (extension) global translation [3], kept in `trans`.
+        Returns a copy of the updated vertices.
+        """
+        if pose_abs is not None:
+            self.pose = pose_abs
+        if pose_pca is not None:
+            n = pose_pca.shape[0]  # AttributeError for a list, like mano_np.py:67
+            if not 0 < n <= 45:
+                raise ValueError(f"pose_pca has {n} coefficients; 0 < N <= 45 (mano_np.py:55-56)")
+            if global_rot is not None:
+                self.rot = np.reshape(global_rot, [1, 3])
+            pose = self.engine.pose_from_pca(self._dev(pose_pca)[None], self._dev(self.rot))
+            self.pose = pose[0].double().cpu().numpy()
+        if shape is not None:
+            self.shape = shape
+        if trans is not None:
+            self.trans = np.reshape(np.asarray(trans, dtype=np.float64), (3,))
+        self.update()
+        return self.verts.copy()
+
+    def update(self):
+        """Recompute every output on the GPU from pose / shape (mano_np.py:79-115)."""
+        pose = np.asarray(self.pose.reshape((-1, 1, 3)), dtype=np.float64)  # list -> AttributeError
+        if pose.size != 3 * self.n_joints:
+            raise ValueError(f"pose has {pose.size} values, {3 * self.n_joints} expected")
+        shape = np.asarray(self.shape, dtype=np.float64)
+        if shape.shape != (self.n_shape_params,):
+            raise ValueError(f"shape has shape {shape.shape}, ({self.n_shape_params},) expected")
+        trans = None if not np.any(self.trans) else self._dev(self.trans)[None]
+        out = self.engine.forward(self._dev(shape)[None], self._dev(pose.reshape(1, self.n_joints, 3)),
+                                  trans, joints=True, rest_verts=True, rest_joints=True, rot_mats=True)
+        host = {k: v[0].double().cpu().numpy() for k, v in out.items()}
+        self.verts = host["verts"]
+        self.rest_verts = host["rest_verts"]
+        self.J = host["rest_joints"]
+        self.R = host["rot_mats"]
+        self.joints = host["joints"]
+
+    def forward_batch(self, betas, pose, trans=None, **kw):
+        """Batched forward on device tensors; see `ManoHip.forward`."""
+        return self.engine.forward(betas, pose, trans, **kw)
+
+    def rodrigues(self, r):
+        """Batched axis-angle [N,1,3] -> rotation [N,3,3] (mano_np.py:117-148), on the GPU."""
+        r = np.asarray(r, dtype=np.float64)
+        return self.engine.rodrigues(self._dev(r.reshape(-1, 3))).double().cpu().numpy()
+
+    def with_zeros(self, x):
+        """Append a [0, 0, 0, 1] row to a [3, 4] matrix (mano_np.py:150-163)."""
+        return np.vstack((x, np.array([[0.0, 0.0, 0.0, 1.0]])))
+
+    def pack(self, x):
+        """[B,4,1] -> [B,4,4] with zero columns in front (mano_np.py:165-179)."""
+        return np.dstack((np.zeros((x.shape[0], 4, 3)), x))
+
+    def export_obj(self, path):
+        """Write `path` and `<stem>_restpose.obj` in the format of mano_np.py:181-201."""
+        write_obj(path, self.verts, self.faces)
+        write_obj(path[:path.index(".obj")] + "_restpose.obj", self.rest_verts, self.faces)
+
+
+def write_obj(path, verts, faces):
+    """OBJ text exactly as mano_np.py:190-194: 'v %f %f %f' and 1-based 'f %d %d %d'."""
+    v = np.asarray(verts, dtype=np.float64).reshape(-1, 3)
+    f = np.asarray(faces).reshape(-1, 3) + 1
+    with open(path, "w") as fp:
+        fp.write("".join("v %f %f %f\n" % (a, b, c) for a, b, c in v))
+        fp.write("".join("f %d %d %d\n" % (a, b, c) for a, b, c in f))

@@ -1,0 +1,64 @@
+"""The C-ABI library loads, exports every symbol include/mano_hip.h declares,
+and rejects bad arguments with status codes -- all without touching a GPU."""
+import ctypes
+
+import pytest
+
+from mano_amd import _abi
+
+
+def test_library_exports_every_header_symbol():
+    lib = _abi.lib()
+    names = _abi.header_functions()
+    assert len(names) >= 13
+    for n in names:
+        assert hasattr(lib, n), n
+        assert n in _abi.SIGNATURES, f"{n} declared in the header but not bound"
+    assert set(_abi.SIGNATURES) == set(names)
+    assert lib.mano_abi_version() == 1
+
+
+def test_library_is_gfx950_code_object():
+    data = open(_abi.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_create_rejects_bad_arguments():
+    lib = _abi.lib()
+    out = ctypes.c_void_p()
+    assert lib.mano_model_create(-1, 778, None, None, None, None, None, None, None, None,
+                                 ctypes.byref(out)) == _abi.MANO_EINVAL
+    assert "negative" in _abi.last_error()
+    assert lib.mano_model_create(0, 778, None, None, None, None, None, None, None, None,
+                                 None) == _abi.MANO_EINVAL
+    assert lib.mano_model_create(0, 0, None, None, None, None, None, None, None, None,
+                                 ctypes.byref(out)) == _abi.MANO_EINVAL
+    assert out.value is None
+
+
+def test_null_handle_paths():
+    lib = _abi.lib()
+    assert lib.mano_workspace_bytes(None, 10) == 0
+    assert lib.mano_model_destroy(None) == _abi.MANO_OK
+    assert lib.mano_forward(None, 1, None, 10, None, None, None, None, None, None, None, None,
+                            0, None) == _abi.MANO_EINVAL
+    assert "NULL" in _abi.last_error()
+    for fn, args in (("mano_stage_blend", (None, 1, None, None, 0, None)),
+                     ("mano_stage_skin", (None, 1, None, None, None, None, 0, None)),
+                     ("mano_pose_from_pca", (None, 1, None, 9, 9, None, 0, None, None))):
+        assert getattr(lib, fn)(*args) == _abi.MANO_EINVAL
+
+
+def test_rodrigues_argument_checks():
+    lib = _abi.lib()
+    assert lib.mano_rodrigues(0, 0, None, None, None) == _abi.MANO_OK  # empty: no launch
+    assert lib.mano_rodrigues(0, -1, None, None, None) == _abi.MANO_EINVAL
+    assert lib.mano_rodrigues(-1, 4, ctypes.c_void_p(16), ctypes.c_void_p(16), None) == _abi.MANO_EINVAL
+
+
+def test_check_raises_with_message():
+    lib = _abi.lib()
+    rc = lib.mano_forward(None, 1, None, 10, None, None, None, None, None, None, None, None, 0, None)
+    with pytest.raises(_abi.ManoError) as ei:
+        _abi.check(rc)
+    assert ei.value.code == _abi.MANO_EINVAL

@@ -1,0 +1,69 @@
+"""Data-parallel sharding and the optional gather, on CPU with gloo (world size 2)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from mano_amd.distributed import all_gather, gather_to_root, shard_range
+
+
+@pytest.mark.parametrize("n,world", [(0, 2), (1, 2), (7, 2), (64, 8), (65536, 8), (1000, 3)])
+def test_shard_range_partitions(n, world):
+    seen = []
+    for r in range(world):
+        a, b = shard_range(n, r, world)
+        assert 0 <= a <= b <= n
+        seen.extend(range(a, b))
+    assert seen == list(range(n))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, n_total, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        a, b = shard_range(n_total, rank, world)
+        # Per-hand values depend only on the global index (shard invariance).
+        shard = torch.arange(a, b, dtype=torch.float32)[:, None, None].expand(b - a, 4, 3).contiguous()
+        shard = shard + torch.tensor([0.0, 0.25, 0.5])
+        full = gather_to_root(shard, n_total, root=0)
+        everyone = all_gather(shard, n_total)
+        q.put((rank, None if full is None else full.numpy(), everyone.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_total", [10, 9])
+def test_gather_world2(n_total):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict()
+    for _ in range(world):
+        rank, full, everyone = q.get(timeout=120)
+        results[rank] = (full, everyone)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    expect = np.arange(n_total, dtype=np.float32)[:, None, None] + np.array([0.0, 0.25, 0.5])
+    expect = np.broadcast_to(expect, (n_total, 4, 3))
+    assert results[1][0] is None
+    assert np.array_equal(results[0][0], expect)
+    for r in range(world):
+        assert np.array_equal(results[r][1], expect)

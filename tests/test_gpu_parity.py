@@ -1,0 +1,307 @@
+"""HIP path vs the float64 oracle and the reference goldens (MI355X only).
+
+Tolerance: max |err| <= 1e-5 m on vertices and joints (north_star: float32
+HIP path vs float64 numpy), 1e-6 on rotation matrices and pose features.
+Every call goes through libmano_hip.so (the C-ABI); nothing here has a CPU
+fallback.
+"""
+import numpy as np
+import pytest
+
+from conftest import step_kwargs
+from oracle import mano_oracle
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+TOL_M = 1e-5
+TOL_R = 1e-6
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def engine(params, dev):
+    from mano_amd import ManoHip
+    m = ManoHip(params, device=0)
+    yield m
+    m.close()
+
+
+def f32(a, dev):
+    return torch.tensor(np.asarray(a), dtype=torch.float32, device=dev)
+
+
+def host(t):
+    return t.double().cpu().numpy()
+
+
+def run(engine, dev, betas, pose, trans=None):
+    out = engine.forward(f32(betas, dev), f32(pose, dev), None if trans is None else f32(trans, dev),
+                         joints=True, rest_verts=True, rest_joints=True, rot_mats=True)
+    torch.cuda.synchronize()
+    return {k: host(v) for k, v in out.items()}
+
+
+def assert_close(got, ref, where=""):
+    for k_got, k_ref, tol in (("verts", "verts", TOL_M), ("joints", "joints", TOL_M),
+                              ("rest_verts", "rest_verts", TOL_M), ("rest_joints", "rest_joints", TOL_M),
+                              ("rot_mats", "rot", TOL_R)):
+        err = np.abs(got[k_got] - ref[k_ref]).max() if got[k_got].size else 0.0
+        assert err <= tol, f"{where} {k_got}: max err {err:.3e} > {tol}"
+
+
+def test_library_is_the_loaded_path(engine):
+    import sys
+    from mano_amd import _abi
+    assert _abi._LIB is not None and _abi.LIB_PATH.endswith("libmano_hip.so")
+    assert "oracle" not in sys.modules.get("mano_amd.model").__dict__
+
+
+def test_batch_golden(engine, dev, golden_batch):
+    g = golden_batch
+    got = run(engine, dev, g["betas"], g["pose"])
+    ref = {"verts": g["verts"], "joints": g["joints"], "rest_verts": g["rest_verts"],
+           "rest_joints": g["J"], "rot": g["R"]}
+    assert_close(got, ref, "golden batch")
+
+
+def test_stateful_script_golden(params, golden_steps):
+    """The drop-in MANOModel replays the reference's set_params script."""
+    from mano_amd import MANOModel
+    manifest, data = golden_steps
+    model = None
+    for entry in manifest:
+        i = entry["step"]
+        if model is None:
+            model = MANOModel.from_params(params, device=0)
+        else:
+            ret = model.set_params(**step_kwargs(entry, data))
+            assert ret.dtype == np.float64 and ret.shape == (778, 3)
+            assert ret is not model.verts and np.array_equal(ret, model.verts)
+        for key, got, tol in (("verts", model.verts, TOL_M), ("J", model.J, TOL_M),
+                              ("R", model.R, TOL_R), ("rest_verts", model.rest_verts, TOL_M),
+                              ("joints", model.joints, TOL_M), ("rot", model.rot, 1e-12),
+                              ("pose", np.reshape(model.pose, (-1, 3)), 1e-5)):
+            err = np.abs(np.asarray(got, dtype=np.float64) - data[f"s{i}_out_{key}"]).max()
+            assert err <= tol, (entry["desc"], key, err)
+
+
+def test_export_obj_demo(params, golden_steps, tmp_path):
+    import os
+    from conftest import GOLDEN
+    from mano_amd import MANOModel
+    manifest, data = golden_steps
+    model = MANOModel.from_params(params, device=0)
+    last = manifest[-1]
+    model.set_params(**step_kwargs(last, data))
+    p = str(tmp_path / "hand.obj")
+    model.export_obj(p)
+    for name in ("hand.obj", "hand_restpose.obj"):
+        a = open(os.path.join(GOLDEN, name)).read().split("\n")
+        b = open(tmp_path / name).read().split("\n")
+        assert len(a) == len(b)
+        va = np.array([[float(x) for x in l.split()[1:]] for l in a if l.startswith("v ")])
+        vb = np.array([[float(x) for x in l.split()[1:]] for l in b if l.startswith("v ")])
+        assert np.abs(va - vb).max() <= 1e-5 + 1e-6
+        assert [l for l in a if l.startswith("f ")] == [l for l in b if l.startswith("f ")]
+
+
+@pytest.mark.parametrize("B", [1, 2, 31, 32, 33, 127, 128, 129, 1000])
+def test_ragged_batches(engine, dev, params, B):
+    rng = np.random.default_rng(B)
+    betas = rng.normal(0, 1, (B, 10))
+    pose = rng.normal(0, 0.5, (B, 16, 3))
+    trans = rng.uniform(-1, 1, (B, 3))
+    got = run(engine, dev, betas, pose, trans)
+    ref = mano_oracle.forward(params, betas, pose, trans)
+    ref["rest_joints"] = ref["rest_joints"]
+    assert_close(got, ref, f"B={B}")
+
+
+@pytest.mark.parametrize("mag", [0.0, 1e-20, 1e-12, 1e-8, 1e-6, 1e-4, 1e-3, 1e-2, 0.1,
+                                 np.pi, 2 * np.pi, 3.0, 6.0, 10.0])
+def test_edge_angles(engine, dev, params, mag):
+    rng = np.random.default_rng(17)
+    B = 64
+    d = rng.normal(size=(B, 16, 3))
+    d /= np.linalg.norm(d, axis=-1, keepdims=True)
+    pose = d * mag
+    betas = rng.normal(0, 1, (B, 10))
+    got = run(engine, dev, betas, pose)
+    ref = mano_oracle.forward(params, betas, pose)
+    assert_close(got, ref, f"|theta|={mag}")
+
+
+def test_uniform_pi_and_axis_aligned(engine, dev, params):
+    rng = np.random.default_rng(3)
+    B = 256
+    pose = rng.uniform(-np.pi, np.pi, (B, 16, 3))
+    pose[:16] = 0.0
+    for i in range(16):
+        pose[i, i, i % 3] = np.pi  # exact half turns about each axis
+    betas = rng.normal(0, 2, (B, 10))
+    got = run(engine, dev, betas, pose)
+    assert_close(got, mano_oracle.forward(params, betas, pose), "uniform pi")
+
+
+def test_shared_betas_stride_zero(engine, dev, params):
+    rng = np.random.default_rng(4)
+    beta = rng.normal(0, 1, 10)
+    pose = rng.normal(0, 0.5, (50, 16, 3))
+    out = engine.forward(f32(beta, dev), f32(pose, dev))
+    ref = mano_oracle.forward(params, beta, pose)
+    assert np.abs(host(out["verts"]) - ref["verts"]).max() <= TOL_M
+
+
+def test_flat48_pose(engine, dev, params):
+    rng = np.random.default_rng(5)
+    pose = rng.normal(0, 0.5, (20, 48))
+    betas = rng.normal(0, 1, (20, 10))
+    out = engine.forward(f32(betas, dev), f32(pose, dev))
+    ref = mano_oracle.forward(params, betas, pose)
+    assert np.abs(host(out["verts"]) - ref["verts"]).max() <= TOL_M
+
+
+def test_stage_intermediates(engine, dev, params):
+    """Each kernel alone: features (R-I), skinning transforms, v_posed."""
+    rng = np.random.default_rng(6)
+    B = 70
+    betas = rng.normal(0, 1, (B, 10))
+    pose = rng.normal(0, 0.7, (B, 16, 3))
+    engine.stage_articulate(f32(betas, dev), f32(pose, dev))
+    engine.stage_blend(B)
+    torch.cuda.synchronize()
+    inter = engine.intermediates(B)
+    ref = mano_oracle.forward(params, betas, pose)
+    # features: decode the MFMA A tiles back to X[h][k]
+    tiles = host(inter["features"])  # (nt, 19, 64, 4)
+    X = np.zeros((tiles.shape[0] * 32, 152))
+    for g in range(19):
+        for q in range(4):
+            s = 4 * g + q
+            X[:, 2 * s] = tiles[:, g, :32, q].reshape(-1)
+            X[:, 2 * s + 1] = tiles[:, g, 32:, q].reshape(-1)
+    X = X[:B]
+    assert np.abs(X[:, :10] - betas).max() < 1e-6
+    feats = mano_oracle.pose_features(ref["rot"])
+    assert np.abs(X[:, 10:145] - feats).max() <= TOL_R
+    assert np.all(X[:, 145:] == 0.0)
+    # transforms: oracle G after rest removal, rows 0..2
+    _, G = mano_oracle.chain(ref["rot"], ref["rest_joints"], params["parents"])
+    assert np.abs(host(inter["transforms"]) - G[:, :, :3, :]).max() <= TOL_M
+    assert np.abs(host(inter["vposed"]) - ref["rest_verts"]).max() <= TOL_M
+
+
+def test_large_batch_sampled(engine, dev, params):
+    """Full C2 size (65,536 hands): sampled hands vs the oracle + properties."""
+    B = 65536
+    g = torch.Generator(device=dev).manual_seed(1001)
+    betas = torch.randn((B, 10), generator=g, device=dev)
+    pose = 0.5 * torch.randn((B, 16, 3), generator=g, device=dev)
+    trans = torch.rand((B, 3), generator=g, device=dev) * 2 - 1
+    out = engine.forward(betas, pose, trans, joints=True)
+    torch.cuda.synchronize()
+    verts = out["verts"]
+    assert torch.isfinite(verts).all()
+    idx = np.random.default_rng(0).choice(B, 256, replace=False)
+    idx = np.concatenate([idx, [0, 31, 32, B - 33, B - 1]])
+    ref = mano_oracle.forward(params, host(betas[idx]), host(pose[idx]), host(trans[idx]))
+    assert np.abs(host(verts[idx]) - ref["verts"]).max() <= TOL_M
+    assert np.abs(host(out["joints"][idx]) - ref["joints"]).max() <= TOL_M
+    # shard invariance: any contiguous split gives bit-identical results
+    for a, b in ((0, 1000), (1000, 40000), (40000, B)):
+        part = engine.forward(betas[a:b].contiguous(), pose[a:b].contiguous(),
+                              trans[a:b].contiguous(), joints=False)
+        assert torch.equal(part["verts"], verts[a:b])
+    # determinism
+    again = engine.forward(betas, pose, trans, joints=False)
+    assert torch.equal(again["verts"], verts)
+
+
+def test_root_rotation_equivariance(engine, dev, params):
+    """Rotating the root rotates every vertex about the root joint (property at size)."""
+    rng = np.random.default_rng(8)
+    B = 4096
+    betas = rng.normal(0, 1, (B, 10))
+    pose = rng.normal(0, 0.5, (B, 16, 3))
+    pose[:, 0] = 0.0
+    base = run(engine, dev, betas, pose)
+    rot = np.array([0.0, 0.0, np.pi / 2])
+    pose2 = pose.copy()
+    pose2[:, 0] = rot
+    turned = run(engine, dev, betas, pose2)
+    Rz = mano_oracle.rodrigues(rot)
+    j0 = base["rest_joints"][:, :1]
+    expect = (base["verts"] - j0) @ Rz.T + j0
+    assert np.abs(turned["verts"] - expect).max() <= 2 * TOL_M
+
+
+def test_empty_batch(engine, dev):
+    out = engine.forward(torch.empty((0, 10), device=dev), torch.empty((0, 16, 3), device=dev))
+    assert out["verts"].shape == (0, 778, 3)
+
+
+@pytest.mark.parametrize("n", [1, 9, 45])
+def test_pose_from_pca(engine, dev, params, n):
+    rng = np.random.default_rng(n)
+    B = 40
+    c = rng.normal(0, 1, (B, n))
+    rot = rng.normal(0, 1, (B, 3))
+    got = host(engine.pose_from_pca(f32(c, dev), f32(rot, dev)))
+    ref = mano_oracle.pose_from_pca(params, c, rot)
+    assert np.abs(got - ref).max() <= 1e-5
+
+
+def test_rodrigues_kernel(engine, dev):
+    rng = np.random.default_rng(9)
+    r = np.concatenate([rng.normal(0, 1, (500, 3)), np.zeros((1, 3)), [[1e-20, 0, 0], [np.pi, 0, 0]]])
+    got = host(engine.rodrigues(f32(r, dev)))
+    assert np.abs(got - mano_oracle.rodrigues(r)).max() <= TOL_R
+
+
+def test_errors(engine, dev):
+    from mano_amd import _abi
+    with pytest.raises(ValueError):
+        engine.forward(torch.zeros((3, 10), device=dev, dtype=torch.float64), torch.zeros((3, 16, 3), device=dev))
+    with pytest.raises(ValueError):
+        engine.forward(torch.zeros((3, 9), device=dev), torch.zeros((3, 16, 3), device=dev))
+    with pytest.raises(ValueError):
+        engine.forward(torch.zeros((3, 10)), torch.zeros((3, 16, 3)))
+    # workspace too small -> MANO_ESMALL through the raw ABI
+    import ctypes
+    lib = _abi.lib()
+    b = torch.zeros((64, 10), device=dev)
+    p = torch.zeros((64, 16, 3), device=dev)
+    v = torch.empty((64, 778, 3), device=dev)
+    ws = torch.empty(1024, dtype=torch.uint8, device=dev)
+    rc = lib.mano_forward(engine._h, 64, ctypes.c_void_p(b.data_ptr()), 10, ctypes.c_void_p(p.data_ptr()),
+                          None, ctypes.c_void_p(v.data_ptr()), None, None, None, None,
+                          ctypes.c_void_p(ws.data_ptr()), 1024, None)
+    assert rc == _abi.MANO_ESMALL and "workspace" in _abi.last_error()
+
+
+def test_dropin_quirks(params):
+    from mano_amd import MANOModel
+    m = MANOModel.from_params(params, device=0)
+    with pytest.raises(ValueError):
+        m.set_params(shape=np.zeros(9))          # mano_np.py:81 dot -> ValueError
+    m.shape = np.zeros(10)
+    with pytest.raises(AttributeError):
+        m.set_params(pose_abs=[[0.0, 0.0, 0.0]] * 16)  # list pose -> AttributeError at :84
+    m.pose = np.zeros((16, 3))
+    with pytest.raises(AttributeError):
+        m.set_params(pose_pca=[0.1, 0.2])         # list pca -> AttributeError at :67
+    # global_rot without pose_pca is ignored (read only on the PCA branch, :70-72)
+    m.set_params(pose_abs=np.zeros((16, 3)), global_rot=[1.0, 0, 0])
+    assert np.all(m.rot == 0)
+    # translation extension: verts shift exactly, joints too
+    v0 = m.verts.copy()
+    j0 = m.joints.copy()
+    m.set_params(trans=[0.1, -0.2, 0.3])
+    assert np.abs(m.verts - v0 - [0.1, -0.2, 0.3]).max() < 1e-6
+    assert np.abs(m.joints - j0 - [0.1, -0.2, 0.3]).max() < 1e-6
