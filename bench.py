@@ -31,6 +31,7 @@ import torch.distributed as dist  # noqa: E402
 V, NCOL, K = 778, 2334, 145
 BLEND_FLOP_PER_HAND = 2 * NCOL * K                 # 676,860
 SKIN_BYTES_PER_HAND = NCOL * 4 * 2 + 16 * 12 * 4   # v_posed in + verts out + transforms = 19,440
+SKIN_FLOP_PER_HAND = V * (16 * 12 * 2 + 9 * 2)     # blend 16 transforms + apply = 312,312
 ARTICULATE_BYTES_PER_HAND = (10 + 48) * 4 + 16 * 12 * 4 + 16 * 3 * 4 + 152 * 4  # in + A + joints + X
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, spec
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -43,6 +44,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=65536, help="hands per GPU per step")
     ap.add_argument("--gather", action="store_true", help="RCCL gather of verts+joints to GPU 0")
+    ap.add_argument("--path", choices=("fused", "unfused"), default="fused",
+                    help="fused: articulate + blend_skin (default); unfused: articulate + blend + skin")
     ap.add_argument("--model", default=None, help="dump_model.py pickle (default: synthetic seed 0)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
@@ -106,18 +109,26 @@ def main():
     model.workspace(B)
     stream = torch.cuda.current_stream(dev)
 
+    fused = args.path == "fused"
+
     def step(evs=None):
         if evs is not None:
             evs[0].record(stream)
         model.stage_articulate(betas, pose, joints=joints)
         if evs is not None:
             evs[1].record(stream)
-        model.stage_blend(B)
-        if evs is not None:
-            evs[2].record(stream)
-        model.stage_skin(B, verts)
-        if evs is not None:
-            evs[3].record(stream)
+        if fused:
+            model.stage_blend_skin(B, verts)
+            if evs is not None:
+                evs[2].record(stream)
+                evs[3].record(stream)
+        else:
+            model.stage_blend(B)
+            if evs is not None:
+                evs[2].record(stream)
+            model.stage_skin(B, verts)
+            if evs is not None:
+                evs[3].record(stream)
         if args.gather and world > 1:
             gather_to_root(verts, B * world, root=0)
             gather_to_root(joints, B * world, root=0)
@@ -142,29 +153,51 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
-    ms = {name: float(np.mean([e[a].elapsed_time(e[b]) for e in events]))
-          for name, a, b in (("articulate", 0, 1), ("blend", 1, 2), ("skin", 2, 3))}
-    kernels = {
-        "articulate": {"ms": ms["articulate"], "bound": "latency",
-                       "achieved_GBs": ARTICULATE_BYTES_PER_HAND * B / (ms["articulate"] * 1e-3) / 1e9},
-        "blend": {"ms": ms["blend"], "bound": "mfma",
-                  "achieved_TFLOPs": BLEND_FLOP_PER_HAND * B / (ms["blend"] * 1e-3) / 1e12},
-        "skin": {"ms": ms["skin"], "bound": "hbm",
-                 "achieved_GBs": SKIN_BYTES_PER_HAND * B / (ms["skin"] * 1e-3) / 1e9},
-    }
-    kernels["blend"]["frac"] = kernels["blend"]["achieved_TFLOPs"] / PEAK_FP32_TFLOPS
-    kernels["skin"]["frac"] = kernels["skin"]["achieved_GBs"] / PEAK_HBM_GBS
-    dominant = "blend" if ms["blend"] >= ms["skin"] else "skin"
-    if dominant == "blend":
-        ach = kernels["blend"]["achieved_TFLOPs"]
-        traffic = load_traffic(args.pmc, "blend", B)
-        roof = {"kernel": "blend_kernel", "bound": "mfma", "achieved": ach, "peak": PEAK_FP32_TFLOPS,
-                "unit": "TFLOP/s", "frac": ach / PEAK_FP32_TFLOPS, "traffic": traffic}
+    def span(a, b, evs):
+        return float(np.mean([e[a].elapsed_time(e[b]) for e in evs]))
+
+    kernels = {"articulate": {"ms": span(0, 1, events), "bound": "latency"}}
+    kernels["articulate"]["achieved_GBs"] = ARTICULATE_BYTES_PER_HAND * B / (kernels["articulate"]["ms"] * 1e-3) / 1e9
+    if fused:
+        ms_bs = span(1, 2, events)
+        ach = BLEND_FLOP_PER_HAND * B / (ms_bs * 1e-3) / 1e12
+        kernels["blend_skin"] = {"ms": ms_bs, "bound": "mfma", "achieved_TFLOPs": ach,
+                                 "frac": ach / PEAK_FP32_TFLOPS,
+                                 "lbs_valu_TFLOPs": SKIN_FLOP_PER_HAND * B / (ms_bs * 1e-3) / 1e12}
+        roof = {"kernel": "blend_skin_kernel", "bound": "mfma", "achieved": ach,
+                "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_FP32_TFLOPS,
+                "traffic": load_traffic(args.pmc, "blend_skin", B)}
+        # The unfused kernels, timed on the same stream after the timed region
+        # (not part of `value`): the standalone MFMA blend and the HBM-bound LBS.
+        uev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(5)]
+        for e in [None] + uev:
+            if e is not None:
+                e[0].record(stream)
+            model.stage_blend(B)
+            if e is not None:
+                e[1].record(stream)
+            model.stage_skin(B, verts)
+            if e is not None:
+                e[2].record(stream)
+        torch.cuda.synchronize()
+        ms_b, ms_s = span(0, 1, uev), span(1, 2, uev)
     else:
-        ach = kernels["skin"]["achieved_GBs"]
-        traffic = load_traffic(args.pmc, "skin", B)
-        roof = {"kernel": "skin_kernel", "bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS,
-                "unit": "GB/s", "frac": ach / PEAK_HBM_GBS, "traffic": traffic}
+        ms_b, ms_s = span(1, 2, events), span(2, 3, events)
+    ach_b = BLEND_FLOP_PER_HAND * B / (ms_b * 1e-3) / 1e12
+    ach_s = SKIN_BYTES_PER_HAND * B / (ms_s * 1e-3) / 1e9
+    kernels["blend"] = {"ms": ms_b, "bound": "mfma", "achieved_TFLOPs": ach_b,
+                        "frac": ach_b / PEAK_FP32_TFLOPS, "in_timed_path": not fused}
+    kernels["skin"] = {"ms": ms_s, "bound": "hbm", "achieved_GBs": ach_s,
+                       "frac": ach_s / PEAK_HBM_GBS, "in_timed_path": not fused}
+    if not fused:
+        if ms_b >= ms_s:
+            roof = {"kernel": "blend_kernel", "bound": "mfma", "achieved": ach_b,
+                    "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": ach_b / PEAK_FP32_TFLOPS,
+                    "traffic": load_traffic(args.pmc, "blend", B)}
+        else:
+            roof = {"kernel": "skin_kernel", "bound": "hbm", "achieved": ach_s, "peak": PEAK_HBM_GBS,
+                    "unit": "GB/s", "frac": ach_s / PEAK_HBM_GBS,
+                    "traffic": load_traffic(args.pmc, "skin", B)}
 
     if rank == 0:
         total = B * world * args.steps
@@ -185,6 +218,7 @@ def main():
             "config": {"workload": "C2: full-pose fp32 MANO forward, 65,536 hands per GPU"
                        if B == 65536 else f"{B} hands per GPU",
                        "hands_per_gpu": B, "global_batch": B * world, "outputs": "verts+joints",
+                       "path": args.path,
                        "gather_to_gpu0": bool(args.gather and world > 1),
                        "parallelism": f"dp{world}"},
             "roofline": roof,

@@ -55,7 +55,7 @@ typedef struct mano_model mano_model; /* opaque, device-resident model buffer */
 /* Upload a model and build its device buffer.
  * Replaces MANOModel.__init__'s array binding (mano_np.py:17-33) for the
  * dump_model.py layout (dump_model.py:8-18).  Host float64 inputs:
- *   mesh_template    [V][3]          mesh_shape_basis [V][3][10]
+ *   mesh_template    [V][3] (V >= 32) mesh_shape_basis [V][3][10]
  *   mesh_pose_basis  [V][3][135]     J_regressor      [16][V] (dense)
  *   skinning_weights [V][16]         parents          [16] int32, -1 at root,
  *                                                     parents[i] < i
@@ -75,8 +75,11 @@ int mano_model_destroy(mano_model* model);
 /* Vertex count and device of a model. */
 int mano_model_info(const mano_model* model, int32_t* n_verts, int32_t* device);
 
-/* Device workspace (bytes) one forward over n_hands needs. */
+/* Device workspace (bytes) for n_hands: `mano_workspace_bytes` covers every
+ * call (the unfused stages keep v_posed in it), `mano_forward_workspace_bytes`
+ * only what mano_forward / articulate / blend_skin use. */
 size_t mano_workspace_bytes(const mano_model* model, int64_t n_hands);
+size_t mano_forward_workspace_bytes(const mano_model* model, int64_t n_hands);
 
 /* Byte offsets of the intermediates inside the workspace (for inspection):
  * pose-feature operand tiles, skinning transforms [n][16][3][4], v_posed. */
@@ -85,9 +88,9 @@ int mano_workspace_offsets(const mano_model* model, int64_t n_hands,
                            size_t* vposed_off);
 
 /* The full forward pass: MANOModel.update() (mano_np.py:79-115) for n_hands
- * independent hands.  verts is required; joints, rest_verts, rest_joints,
- * rot_mats and trans are nullable.  With rest_verts == NULL the v_posed
- * intermediate lives in the workspace. */
+ * independent hands = articulate + blend_skin.  verts is required; joints,
+ * rest_verts, rest_joints, rot_mats and trans are nullable.  v_posed never
+ * touches HBM unless rest_verts is requested. */
 int mano_forward(const mano_model* model, int64_t n_hands,
                  const float* betas, int64_t betas_stride, const float* pose,
                  const float* trans, float* verts, float* joints,
@@ -111,6 +114,11 @@ int mano_stage_blend(const mano_model* model, int64_t n_hands, float* rest_verts
 int mano_stage_skin(const mano_model* model, int64_t n_hands,
                     const float* rest_verts, const float* trans, float* verts,
                     void* workspace, size_t workspace_bytes, void* stream);
+/*  blend_skin: blend + skin fused (the LBS runs in the GEMM epilogue, v_posed
+ *              stays on chip; written to rest_verts only when non-NULL). */
+int mano_stage_blend_skin(const mano_model* model, int64_t n_hands, float* rest_verts,
+                          const float* trans, float* verts, void* workspace,
+                          size_t workspace_bytes, void* stream);
 
 /* set_params' PCA branch (mano_np.py:66-72) on device:
  *   pose[h] = [ rot[h] | pca[h][:n_comps] . pose_pca_basis[:n_comps] + mean ]

@@ -10,6 +10,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <new>
 #include <string>
 #include <vector>
@@ -63,12 +64,16 @@ int check_model(const mano_model* m) {
   return MANO_OK;
 }
 
-int check_workspace(const mano_model* m, int64_t n, const void* ws, size_t ws_bytes) {
+// `full`: the unfused stages need the v_posed region too; the fused forward
+// only the feature tiles and skinning transforms.
+int check_workspace(const mano_model* m, int64_t n, const void* ws, size_t ws_bytes,
+                    bool full = true) {
   const mano::Workspace w = mano::workspace_layout(m->dm, n);
+  const size_t need = full ? w.total : w.vposed_off;
   if (!ws) return fail(MANO_EINVAL, "workspace is NULL");
-  if (ws_bytes < w.total)
+  if (ws_bytes < need)
     return fail(MANO_ESMALL, "workspace has %zu bytes, %zu needed for %lld hands", ws_bytes,
-                w.total, (long long)n);
+                need, (long long)n);
   if (reinterpret_cast<uintptr_t>(ws) % 256 != 0)
     return fail(MANO_EINVAL, "workspace must be 256-byte aligned");
   return MANO_OK;
@@ -94,7 +99,8 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   if (!out) return fail(MANO_EINVAL, "out is NULL");
   *out = nullptr;
   if (device < 0) return fail(MANO_EINVAL, "device %d is negative", device);
-  if (n_verts <= 0 || n_verts > (1 << 24)) return fail(MANO_EINVAL, "n_verts %d out of range", n_verts);
+  if (n_verts < 32 || n_verts > (1 << 24))
+    return fail(MANO_EINVAL, "n_verts %d out of range [32, 2^24]", n_verts);
   if (!mesh_template || !mesh_shape_basis || !mesh_pose_basis || !j_regressor ||
       !skinning_weights || !parents)
     return fail(MANO_EINVAL, "a required model array is NULL");
@@ -155,11 +161,39 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
           }
           tiles[((size_t(t) * kKGroups + g) * 64 + l) * 4 + q] = v;
         }
+  // Fused blend+skin layout: group g = 32 vertices starting at min(32g, V-32);
+  // its three tiles hold the x, y, z columns of those vertices.
+  const int n_groups = (V + 31) / 32;
+  std::vector<float> gtiles(size_t(n_groups) * 3 * kTileFloats, 0.f);
+  std::vector<float> gtmpl(size_t(n_groups) * 3 * kColTile, 0.f);
+  for (int g = 0; g < n_groups; ++g) {
+    const int vb = std::max(0, std::min(32 * g, V - 32));
+    for (int q = 0; q < 3; ++q) {
+      const size_t t = size_t(g) * 3 + q;
+      for (int c = 0; c < kColTile; ++c) {
+        const int v = vb + c;
+        if (v < V) gtmpl[t * kColTile + c] = float(mesh_template[size_t(v) * 3 + q]);
+      }
+      for (int gg = 0; gg < kKGroups; ++gg)
+        for (int l = 0; l < 64; ++l)
+          for (int qq = 0; qq < 4; ++qq) {
+            const int k = 2 * (4 * gg + qq) + (l >> 5);
+            const int v = vb + (l & 31);
+            float val = 0.f;
+            if (k < kK && v < V) {
+              const size_t colv = size_t(v) * 3 + q;
+              val = k < kShape ? float(mesh_shape_basis[colv * kShape + k])
+                               : float(mesh_pose_basis[colv * kPoseFeats + (k - kShape)]);
+            }
+            gtiles[((t * kKGroups + gg) * 64 + l) * 4 + qq] = val;
+          }
+    }
+  }
   std::vector<float> tmpl(size_t(n_col_tiles) * kColTile, 0.f);
   for (int i = 0; i < n_cols; ++i) tmpl[i] = float(mesh_template[i]);
   std::vector<float> wts(size_t(V) * kJoints);
   for (size_t i = 0; i < wts.size(); ++i) wts[i] = float(skinning_weights[i]);
-  std::vector<float> pca(kPca * kPca, 0.f), pmean(kPca, 0.f);
+  std::vector<float> pca(kPca * kPca, 0.f), pmean(kPca, 0.f), zeros(64, 0.f);
   if (pose_pca_basis) {
     for (int i = 0; i < kPca * kPca; ++i) pca[i] = float(pose_pca_basis[i]);
     for (int i = 0; i < kPca; ++i) pmean[i] = float(pose_pca_mean[i]);
@@ -172,7 +206,8 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
       {wts.data(), wts.size() * 4, 0},     {jt.data(), jt.size() * 4, 0},
       {js.data(), js.size() * 4, 0},       {parents, kJoints * 4, 0},
       {depth.data(), kJoints * 4, 0},      {pca.data(), pca.size() * 4, 0},
-      {pmean.data(), pmean.size() * 4, 0}};
+      {pmean.data(), pmean.size() * 4, 0}, {zeros.data(), zeros.size() * 4, 0},
+      {gtiles.data(), gtiles.size() * 4, 0}, {gtmpl.data(), gtmpl.size() * 4, 0}};
   size_t total = 0;
   for (auto& p : parts) {
     p.off = total;
@@ -206,6 +241,10 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   m->dm.depth = reinterpret_cast<int32_t*>(b + parts[6].off);
   m->dm.pca_basis = reinterpret_cast<float*>(b + parts[7].off);
   m->dm.pca_mean = reinterpret_cast<float*>(b + parts[8].off);
+  m->dm.zeros = reinterpret_cast<float*>(b + parts[9].off);
+  m->dm.basis_groups = reinterpret_cast<float*>(b + parts[10].off);
+  m->dm.template_groups = reinterpret_cast<float*>(b + parts[11].off);
+  m->dm.n_groups = n_groups;
   m->dm.max_depth = max_depth;
   m->dm.n_verts = V;
   m->dm.n_cols = n_cols;
@@ -238,6 +277,11 @@ size_t mano_workspace_bytes(const mano_model* m, int64_t n) {
   return mano::workspace_layout(m->dm, n).total;
 }
 
+size_t mano_forward_workspace_bytes(const mano_model* m, int64_t n) {
+  if (check_model(m) || n < 0) return 0;
+  return mano::workspace_layout(m->dm, n).vposed_off;
+}
+
 int mano_workspace_offsets(const mano_model* m, int64_t n, size_t* features_off,
                            size_t* transforms_off, size_t* vposed_off) {
   if (int rc = check_model(m)) return rc;
@@ -259,7 +303,7 @@ int mano_stage_articulate(const mano_model* m, int64_t n, const float* betas,
   if (!betas || !pose) return fail(MANO_EINVAL, "betas and pose are required");
   if (betas_stride != 0 && betas_stride < mano::kShape)
     return fail(MANO_EINVAL, "betas_stride %lld must be 0 or >= 10", (long long)betas_stride);
-  if (int rc = check_workspace(m, n, ws, ws_bytes)) return rc;
+  if (int rc = check_workspace(m, n, ws, ws_bytes, false)) return rc;
   DeviceGuard guard(m->device);
   if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
   const mano::Workspace w = mano::workspace_layout(m->dm, n);
@@ -308,6 +352,25 @@ int mano_stage_skin(const mano_model* m, int64_t n, const float* rest_verts, con
   return MANO_OK;
 }
 
+int mano_stage_blend_skin(const mano_model* m, int64_t n, float* rest_verts, const float* trans,
+                          float* verts, void* ws, size_t ws_bytes, void* stream) {
+  if (int rc = check_model(m)) return rc;
+  if (n < 0 || n > kMaxHands) return fail(MANO_EINVAL, "n_hands %lld out of range", (long long)n);
+  if (n == 0) return MANO_OK;
+  if (!verts) return fail(MANO_EINVAL, "verts is required");
+  if (int rc = check_workspace(m, n, ws, ws_bytes, false)) return rc;
+  DeviceGuard guard(m->device);
+  if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
+  const mano::Workspace w = mano::workspace_layout(m->dm, n);
+  char* base = static_cast<char*>(ws);
+  hipError_t e = mano::launch_blend_skin(
+      m->dm, n, reinterpret_cast<const float*>(base + w.features_off),
+      reinterpret_cast<const float*>(base + w.transforms_off), trans, verts, rest_verts,
+      static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "blend_skin launch");
+  return MANO_OK;
+}
+
 int mano_forward(const mano_model* m, int64_t n, const float* betas, int64_t betas_stride,
                  const float* pose, const float* trans, float* verts, float* joints,
                  float* rest_verts, float* rest_joints, float* rot_mats, void* ws,
@@ -318,8 +381,7 @@ int mano_forward(const mano_model* m, int64_t n, const float* betas, int64_t bet
   if (int rc = mano_stage_articulate(m, n, betas, betas_stride, pose, trans, joints, rest_joints,
                                      rot_mats, ws, ws_bytes, stream))
     return rc;
-  if (int rc = mano_stage_blend(m, n, rest_verts, ws, ws_bytes, stream)) return rc;
-  return mano_stage_skin(m, n, rest_verts, trans, verts, ws, ws_bytes, stream);
+  return mano_stage_blend_skin(m, n, rest_verts, trans, verts, ws, ws_bytes, stream);
 }
 
 int mano_pose_from_pca(const mano_model* m, int64_t n, const float* pca, int32_t n_comps,

@@ -35,10 +35,14 @@ struct DeviceModel {
   int32_t* depth;       // [16] depth in the kinematic tree (root 0)
   float* pca_basis;     // [45][45]
   float* pca_mean;      // [45]
+  float* zeros;         // [64] zero vector (stand-in operand for an absent trans)
+  float* basis_groups;  // [n_groups][3][kKGroups][64][4] B tiles: x|y|z of 32 verts
+  float* template_groups; // [n_groups][3][32] template coordinate per group column
   int32_t max_depth;
   int32_t n_verts;
   int32_t n_cols;       // 3V
   int32_t n_col_tiles;  // ceil(3V / 32)
+  int32_t n_groups;     // ceil(V / 32) vertex groups of the fused kernel (last one shifted)
 };
 
 // Workspace carving (all offsets 256-B aligned).
@@ -65,6 +69,9 @@ hipError_t launch_articulate(const DeviceModel& m, int64_t n, const float* betas
                              float* rest_joints, float* rot_mats, hipStream_t stream);
 hipError_t launch_blend(const DeviceModel& m, int64_t n, const float* features,
                         float* vposed, hipStream_t stream);
+hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features,
+                             const float* transforms, const float* trans, float* verts,
+                             float* vposed, hipStream_t stream);
 hipError_t launch_skin(const DeviceModel& m, int64_t n, const float* transforms,
                        const float* vposed, const float* trans, float* verts,
                        hipStream_t stream);

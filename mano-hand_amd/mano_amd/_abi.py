@@ -44,6 +44,7 @@ SIGNATURES = {
     "mano_model_destroy": (ctypes.c_int, [_p]),
     "mano_model_info": (ctypes.c_int, [_p, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
     "mano_workspace_bytes": (ctypes.c_size_t, [_p, _i64]),
+    "mano_forward_workspace_bytes": (ctypes.c_size_t, [_p, _i64]),
     "mano_workspace_offsets": (ctypes.c_int, [_p, _i64, ctypes.POINTER(ctypes.c_size_t),
                                               ctypes.POINTER(ctypes.c_size_t),
                                               ctypes.POINTER(ctypes.c_size_t)]),
@@ -53,6 +54,7 @@ SIGNATURES = {
                                              ctypes.c_size_t, _p]),
     "mano_stage_blend": (ctypes.c_int, [_p, _i64, _p, _p, ctypes.c_size_t, _p]),
     "mano_stage_skin": (ctypes.c_int, [_p, _i64, _p, _p, _p, _p, ctypes.c_size_t, _p]),
+    "mano_stage_blend_skin": (ctypes.c_int, [_p, _i64, _p, _p, _p, _p, ctypes.c_size_t, _p]),
     "mano_pose_from_pca": (ctypes.c_int, [_p, _i64, _p, _i32, _i64, _p, _i64, _p, _p]),
     "mano_rodrigues": (ctypes.c_int, [ctypes.c_int, _i64, _p, _p, _p]),
 }

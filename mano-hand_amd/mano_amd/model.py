@@ -199,6 +199,14 @@ class ManoHip:
                                               _ptr(verts), ws, wsb,
                                               _stream_handle(self.device, stream)))
 
+    def stage_blend_skin(self, n: int, verts: torch.Tensor, rest_verts=None, trans=None,
+                         stream=None):
+        """Fused blend GEMM + LBS (the second half of `forward`)."""
+        ws, wsb = self._ws_args(n)
+        _abi.check(_abi.lib().mano_stage_blend_skin(self._h, n, _ptr(rest_verts), _ptr(trans),
+                                                    _ptr(verts), ws, wsb,
+                                                    _stream_handle(self.device, stream)))
+
     def intermediates(self, n: int) -> Dict[str, torch.Tensor]:
         """Views of the workspace after a stage/forward call over `n` hands:
         `features` (ceil(n/32), 19, 64, 4) MFMA A tiles, `transforms`

@@ -305,3 +305,23 @@ def test_dropin_quirks(params):
     m.set_params(trans=[0.1, -0.2, 0.3])
     assert np.abs(m.verts - v0 - [0.1, -0.2, 0.3]).max() < 1e-6
     assert np.abs(m.joints - j0 - [0.1, -0.2, 0.3]).max() < 1e-6
+
+
+@pytest.mark.parametrize("B", [1, 33, 200, 4096])
+def test_fused_equals_unfused(engine, dev, params, B):
+    """blend_skin (fused, v_posed on chip) == blend then skin, bit for bit."""
+    rng = np.random.default_rng(100 + B)
+    betas = f32(rng.normal(0, 1, (B, 10)), dev)
+    pose = f32(rng.normal(0, 0.6, (B, 16, 3)), dev)
+    trans = f32(rng.uniform(-1, 1, (B, 3)), dev)
+    fused = engine.forward(betas, pose, trans, rest_verts=True)
+    engine.stage_articulate(betas, pose, trans)
+    vp = torch.empty((B, 778, 3), device=dev)
+    v = torch.empty((B, 778, 3), device=dev)
+    engine.stage_blend(B, rest_verts=vp)
+    engine.stage_skin(B, v, rest_verts=vp, trans=trans)
+    torch.cuda.synchronize()
+    assert torch.equal(fused["rest_verts"], vp)
+    assert torch.equal(fused["verts"], v)
+    ref = mano_oracle.forward(params, host(betas), host(pose), host(trans))
+    assert np.abs(host(v) - ref["verts"]).max() <= TOL_M
