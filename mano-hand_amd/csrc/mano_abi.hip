@@ -153,11 +153,13 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
           const int k = 2 * (4 * g + q) + (l >> 5);
           const int col = t * kColTile + (l & 31);
           float v = 0.f;
-          if (k < kK && col < n_cols) {
+          if (col < n_cols) {
             if (k < kShape)
               v = float(mesh_shape_basis[size_t(col) * kShape + k]);
-            else
+            else if (k < kK)
               v = float(mesh_pose_basis[size_t(col) * kPoseFeats + (k - kShape)]);
+            else if (k == kK)
+              v = float(mesh_template[col]);  // multiplied by X[:, 145] = 1
           }
           tiles[((size_t(t) * kKGroups + g) * 64 + l) * 4 + q] = v;
         }
@@ -180,14 +182,26 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
             const int k = 2 * (4 * gg + qq) + (l >> 5);
             const int v = vb + (l & 31);
             float val = 0.f;
-            if (k < kK && v < V) {
+            if (k <= kK && v < V) {
               const size_t colv = size_t(v) * 3 + q;
               val = k < kShape ? float(mesh_shape_basis[colv * kShape + k])
-                               : float(mesh_pose_basis[colv * kPoseFeats + (k - kShape)]);
+                    : k < kK   ? float(mesh_pose_basis[colv * kPoseFeats + (k - kShape)])
+                               : float(mesh_template[colv]);  // row 145: template
             }
             gtiles[((t * kKGroups + gg) * 64 + l) * 4 + qq] = val;
           }
     }
+  }
+  std::vector<float> wfr(size_t(n_groups) * kWFragFloats, 0.f);
+  for (int g = 0; g < n_groups; ++g) {
+    const int vb = std::max(0, std::min(32 * g, V - 32));
+    for (int l = 0; l < 64; ++l)
+      for (int st = 0; st < 8; ++st) {
+        const int v = vb + (l & 31), jj = 2 * st + (l >> 5);
+        if (v < V)
+          wfr[size_t(g) * kWFragFloats + ((st >> 2) * 64 + l) * 4 + (st & 3)] =
+              float(skinning_weights[size_t(v) * kJoints + jj]);
+      }
   }
   std::vector<float> tmpl(size_t(n_col_tiles) * kColTile, 0.f);
   for (int i = 0; i < n_cols; ++i) tmpl[i] = float(mesh_template[i]);
@@ -207,7 +221,8 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
       {js.data(), js.size() * 4, 0},       {parents, kJoints * 4, 0},
       {depth.data(), kJoints * 4, 0},      {pca.data(), pca.size() * 4, 0},
       {pmean.data(), pmean.size() * 4, 0}, {zeros.data(), zeros.size() * 4, 0},
-      {gtiles.data(), gtiles.size() * 4, 0}, {gtmpl.data(), gtmpl.size() * 4, 0}};
+      {gtiles.data(), gtiles.size() * 4, 0}, {gtmpl.data(), gtmpl.size() * 4, 0},
+      {wfr.data(), wfr.size() * 4, 0}};
   size_t total = 0;
   for (auto& p : parts) {
     p.off = total;
@@ -244,6 +259,7 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   m->dm.zeros = reinterpret_cast<float*>(b + parts[9].off);
   m->dm.basis_groups = reinterpret_cast<float*>(b + parts[10].off);
   m->dm.template_groups = reinterpret_cast<float*>(b + parts[11].off);
+  m->dm.weight_frags = reinterpret_cast<float*>(b + parts[12].off);
   m->dm.n_groups = n_groups;
   m->dm.max_depth = max_depth;
   m->dm.n_verts = V;
@@ -310,7 +326,8 @@ int mano_stage_articulate(const mano_model* m, int64_t n, const float* betas,
   char* base = static_cast<char*>(ws);
   hipError_t e = mano::launch_articulate(
       m->dm, n, betas, betas_stride, pose, trans, reinterpret_cast<float*>(base + w.features_off),
-      reinterpret_cast<float*>(base + w.transforms_off), joints, rest_joints, rot_mats,
+      reinterpret_cast<float*>(base + w.transforms_off),
+      reinterpret_cast<float*>(base + w.tfrag_off), joints, rest_joints, rot_mats,
       static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "articulate launch");
   return MANO_OK;
@@ -365,7 +382,7 @@ int mano_stage_blend_skin(const mano_model* m, int64_t n, float* rest_verts, con
   char* base = static_cast<char*>(ws);
   hipError_t e = mano::launch_blend_skin(
       m->dm, n, reinterpret_cast<const float*>(base + w.features_off),
-      reinterpret_cast<const float*>(base + w.transforms_off), trans, verts, rest_verts,
+      reinterpret_cast<const float*>(base + w.tfrag_off), trans, verts, rest_verts,
       static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "blend_skin launch");
   return MANO_OK;

@@ -23,6 +23,12 @@ constexpr int kTileFloats = kKGroups * 64 * 4; // 4864 floats = 19,456 B per til
 constexpr int kHandTile = 32;                  // hands per MFMA row tile
 constexpr int kColTile = 32;                   // basis columns per MFMA col tile
 constexpr int kTransformFloats = kJoints * 12; // 3x4 skinning transform per joint
+// Fused-kernel LBS operands.  T_{c,k}[hand][v] = sum_j A_j(hand)[c][k] W[v][j]
+// is one 32x32 MFMA tile per (c, k) over K = 16 joints (8 steps of 32x32x2):
+//   A fragments, per hand tile: [c*4+k][s/4][lane][s%4] = A_{2s+(lane>>5)}(32 ht + (lane&31))[c][k]
+//   W fragments, per vertex group: [s/4][lane][s%4]     = W[vb + (lane&31)][2s + (lane>>5)]
+constexpr int kTFragFloats = 12 * 8 * 64;      // 6144 floats = 24 KB per hand tile
+constexpr int kWFragFloats = 8 * 64;           // 512 floats per vertex group
 
 // Device-resident model buffer (float32, layouts chosen for the kernels).
 struct DeviceModel {
@@ -38,6 +44,7 @@ struct DeviceModel {
   float* zeros;         // [64] zero vector (stand-in operand for an absent trans)
   float* basis_groups;  // [n_groups][3][kKGroups][64][4] B tiles: x|y|z of 32 verts
   float* template_groups; // [n_groups][3][32] template coordinate per group column
+  float* weight_frags;  // [n_groups][kWFragFloats] MFMA B fragments of W^T per group
   int32_t max_depth;
   int32_t n_verts;
   int32_t n_cols;       // 3V
@@ -47,7 +54,7 @@ struct DeviceModel {
 
 // Workspace carving (all offsets 256-B aligned).
 struct Workspace {
-  size_t features_off, transforms_off, vposed_off, total;
+  size_t features_off, transforms_off, tfrag_off, vposed_off, total;
 };
 
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -57,7 +64,8 @@ inline Workspace workspace_layout(const DeviceModel& m, int64_t n) {
   const int64_t n_tiles = (n + kHandTile - 1) / kHandTile;
   w.features_off = 0;
   w.transforms_off = align256(w.features_off + size_t(n_tiles) * kTileFloats * sizeof(float));
-  w.vposed_off = align256(w.transforms_off + size_t(n) * kTransformFloats * sizeof(float));
+  w.tfrag_off = align256(w.transforms_off + size_t(n) * kTransformFloats * sizeof(float));
+  w.vposed_off = align256(w.tfrag_off + size_t(n_tiles) * kTFragFloats * sizeof(float));
   w.total = align256(w.vposed_off + size_t(n) * m.n_cols * sizeof(float));
   return w;
 }
@@ -65,12 +73,12 @@ inline Workspace workspace_layout(const DeviceModel& m, int64_t n) {
 // Kernel launchers (mano_kernels.hip).  All asynchronous on `stream`.
 hipError_t launch_articulate(const DeviceModel& m, int64_t n, const float* betas,
                              int64_t betas_stride, const float* pose, const float* trans,
-                             float* features, float* transforms, float* joints,
+                             float* features, float* transforms, float* tfrags, float* joints,
                              float* rest_joints, float* rot_mats, hipStream_t stream);
 hipError_t launch_blend(const DeviceModel& m, int64_t n, const float* features,
                         float* vposed, hipStream_t stream);
 hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features,
-                             const float* transforms, const float* trans, float* verts,
+                             const float* tfrags, const float* trans, float* verts,
                              float* vposed, hipStream_t stream);
 hipError_t launch_skin(const DeviceModel& m, int64_t n, const float* transforms,
                        const float* vposed, const float* trans, float* verts,

@@ -67,10 +67,12 @@ __global__ __launch_bounds__(512) void articulate_kernel(
     const float* __restrict__ trans, const float* __restrict__ joint_template,
     const float* __restrict__ joint_shape, const int32_t* __restrict__ parents,
     const int32_t* __restrict__ depth, int max_depth, int64_t n,
-    float* __restrict__ features, float* __restrict__ transforms, float* __restrict__ joints,
-    float* __restrict__ rest_joints, float* __restrict__ rot_mats) {
+    float* __restrict__ features, float* __restrict__ transforms, float* __restrict__ tfrags,
+    float* __restrict__ joints, float* __restrict__ rest_joints, float* __restrict__ rot_mats) {
   __shared__ f32x4 tile[kKGroups * 64];
+  __shared__ f32x4 ttile[kTFragFloats / 4];
   float* tilef = reinterpret_cast<float*>(tile);
+  float* ttilef = reinterpret_cast<float*>(ttile);
 
   const int tid = threadIdx.x;
   const int j = tid & (kJoints - 1);
@@ -140,16 +142,26 @@ __global__ __launch_bounds__(512) void articulate_kernel(
     }
   }
 
+  // Skinning transform A_j = [Rw | t - Rw J] (rest-pose removal, :106-110).
+  float Aj[12];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    Aj[r * 4 + 0] = Rw[r * 3 + 0];
+    Aj[r * 4 + 1] = Rw[r * 3 + 1];
+    Aj[r * 4 + 2] = Rw[r * 3 + 2];
+    Aj[r * 4 + 3] = t[r] - (Rw[r * 3 + 0] * J[0] + Rw[r * 3 + 1] * J[1] + Rw[r * 3 + 2] * J[2]);
+  }
+  // ... and in the fused kernel's MFMA A-fragment layout (mano_internal.h).
+  {
+    const int s = j >> 1;
+    const int ln = hl + 32 * (j & 1);
+#pragma unroll
+    for (int ck = 0; ck < 12; ++ck) ttilef[((ck * 2 + (s >> 2)) * 64 + ln) * 4 + (s & 3)] = Aj[ck];
+  }
   if (valid) {
-    // Skinning transform A_j = [Rw | t - Rw J] (rest-pose removal, :106-110).
     float* A = transforms + h * kTransformFloats + j * 12;
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      A[r * 4 + 0] = Rw[r * 3 + 0];
-      A[r * 4 + 1] = Rw[r * 3 + 1];
-      A[r * 4 + 2] = Rw[r * 3 + 2];
-      A[r * 4 + 3] = t[r] - (Rw[r * 3 + 0] * J[0] + Rw[r * 3 + 1] * J[1] + Rw[r * 3 + 2] * J[2]);
-    }
+    for (int m = 0; m < 12; ++m) A[m] = Aj[m];
     if (joints) {
       float* o = joints + h * (kJoints * 3) + 3 * j;
 #pragma unroll
@@ -168,7 +180,8 @@ __global__ __launch_bounds__(512) void articulate_kernel(
   }
 
   // Blend-GEMM A operand: X[h][k], k < 10 beta, 10 <= k < 145 features
-  // (k = 10 + 9(j-1) + 3 row + col, the ravel order of :91), zeros up to 152.
+  // (k = 10 + 9(j-1) + 3 row + col, the ravel order of :91), X[h][145] = 1
+  // (selects the template row of the basis), zeros up to 152.
   // Fragment layout for v_mfma_f32_32x32x2_f32: step s = k/2 holds
   // X[hand = lane & 31][k = 2s + (lane >> 5)]; 4 steps packed per float4.
   auto put = [&](int k, float v) {
@@ -179,8 +192,9 @@ __global__ __launch_bounds__(512) void articulate_kernel(
   if (j == 0) {
 #pragma unroll
     for (int s = 0; s < kShape; ++s) put(s, beta[s]);
+    put(kK, 1.f);  // X[:, 145] = 1 multiplies the template row of the basis
 #pragma unroll
-    for (int k = kK; k < kKGroups * 8; ++k) put(k, 0.f);
+    for (int k = kK + 1; k < kKGroups * 8; ++k) put(k, 0.f);
   } else {
 #pragma unroll
     for (int m = 0; m < 9; ++m) put(kShape + 9 * (j - 1) + m, rm[m]);
@@ -188,25 +202,60 @@ __global__ __launch_bounds__(512) void articulate_kernel(
   __syncthreads();
   f32x4* dst = reinterpret_cast<f32x4*>(features + int64_t(blockIdx.x) * kTileFloats);
   for (int i = tid; i < kKGroups * 64; i += 512) dst[i] = tile[i];
+  f32x4* tdst = reinterpret_cast<f32x4*>(tfrags + int64_t(blockIdx.x) * kTFragFloats);
+  for (int i = tid; i < kTFragFloats / 4; i += 512) tdst[i] = ttile[i];
 }
 
 // ---------------------------------------------------------------------------
 // blend: 256 threads = 4 waves x 32 hands; loop over all 32-column tiles.
 // ---------------------------------------------------------------------------
+template <int kWaves = 4>
 __device__ __forceinline__ void stage_basis_tile(const float* __restrict__ basis_tiles, int t,
                                                  f32x4* buf, int wave, int lane) {
   const float* src = basis_tiles + int64_t(t) * kTileFloats + lane * 4;
-  for (int g = wave; g < kKGroups; g += 4) {
+  for (int g = wave; g < kKGroups; g += kWaves) {
     __builtin_amdgcn_global_load_lds(
         (const __attribute__((address_space(1))) void*)(src + g * 256),
         (__attribute__((address_space(3))) void*)(buf + g * 64), 16, 0, 0);
   }
 }
 
+__device__ __forceinline__ f32x16 mfma_tile(const float (&a)[kKGroups * 4], const f32x4* __restrict__ b,
+                                            int lane) {
+  // 73 dependent MFMAs (one accumulator; the 64-cycle dependent latency equals
+  // the issue interval).  The LDS read of K-group g+1 is issued before the
+  // four MFMAs of group g and pinned there with a scheduling barrier, so its
+  // latency hides under them (hipcc otherwise sinks it to a wait per group).
+  f32x16 acc = {};
+  f32x4 bn = b[lane];
+#pragma unroll
+  for (int g = 0; g < kKGroups; ++g) {
+    const f32x4 bv = bn;
+    if (g + 1 < kKGroups) bn = b[(g + 1) * 64 + lane];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (4 * g + q < kKSteps) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * g + q], bv[q], acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+__device__ __forceinline__ void store_vposed_tile(float* __restrict__ vposed, const f32x16& acc,
+                                                  int64_t h0, int col, int64_t n, int n_cols,
+                                                  int hi) {
+  // D[hand][col]: col = lane & 31, hand = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
+  if (col < n_cols) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t h = h0 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+      if (h < n) vposed[h * n_cols + col] = acc[r];
+    }
+  }
+}
+
 __global__ __launch_bounds__(256, 2) void blend_kernel(
     const float* __restrict__ features, const float* __restrict__ basis_tiles,
-    const float* __restrict__ template_cols, float* __restrict__ vposed, int64_t n,
-    int n_cols, int n_col_tiles) {
+    float* __restrict__ vposed, int64_t n, int n_cols, int n_col_tiles) {
   __shared__ f32x4 bs[2][kKGroups * 64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -219,7 +268,7 @@ __global__ __launch_bounds__(256, 2) void blend_kernel(
     const f32x4* src = reinterpret_cast<const f32x4*>(features + (active ? ht : 0) * kTileFloats) + lane;
 #pragma unroll
     for (int g = 0; g < kKGroups; ++g) {
-      const f32x4 v = active ? src[g * 64] : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 v = src[g * 64];
       a[4 * g + 0] = v[0];
       a[4 * g + 1] = v[1];
       a[4 * g + 2] = v[2];
@@ -232,116 +281,69 @@ __global__ __launch_bounds__(256, 2) void blend_kernel(
 
   const int hi = lane >> 5;
   const int col_in_tile = lane & 31;
+  const int64_t h0 = ht * kHandTile;
+  // The template is row k = 145 of the basis (X[:, 145] = 1), so the MFMA chain
+  // yields v_posed directly.  Tile t's stores are issued one iteration late,
+  // before tile t+2's LDS-DMA, so the barrier's vmcnt(0) only waits on old
+  // stores and the DMA the MFMA chain has already hidden.
+  f32x16 prev = {};
   for (int t = 0; t < n_col_tiles; ++t) {
+    if (active && t > 0) store_vposed_tile(vposed, prev, h0, (t - 1) * kColTile + col_in_tile, n, n_cols, hi);
     if (t + 1 < n_col_tiles) stage_basis_tile(basis_tiles, t + 1, bs[(t + 1) & 1], wave, lane);
-    const f32x4* b = bs[t & 1];
-    f32x16 acc = {};
-#pragma unroll
-    for (int g = 0; g < kKGroups; ++g) {
-      const f32x4 bv = b[g * 64 + lane];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (4 * g + q < kKSteps) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * g + q], bv[q], acc, 0, 0, 0);
-      }
-    }
-    // D[hand][col]: col = lane & 31, hand = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
-    const int col = t * kColTile + col_in_tile;
-    if (active && col < n_cols) {
-      const float tv = template_cols[col];
-      const int64_t h0 = ht * kHandTile;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t h = h0 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-        if (h < n) vposed[h * n_cols + col] = acc[r] + tv;
-      }
-    }
+    prev = mfma_tile(a, bs[t & 1], lane);
     __syncthreads();
   }
+  if (active) store_vposed_tile(vposed, prev, h0, (n_col_tiles - 1) * kColTile + col_in_tile, n, n_cols, hi);
 }
 
 // ---------------------------------------------------------------------------
 // blend_skin: the blend GEMM with LBS fused behind it.
 //
-// One 768-thread block = 4 "M" waves + 8 "S" waves (one M and two S per SIMD),
-// 128 hands.  M wave w keeps its 32 hands' A fragments in VGPRs and runs the
-// MFMA chains; the block's four M waves share each basis tile, staged in LDS by
-// LDS-DMA (double-buffered, one barrier per tile).  Vertices come in groups of
-// 32 whose basis columns are packed as three tiles (x, y, z of the same 32
-// vertices), so after a group's three tiles lane l of M wave w holds the full
-// v_posed point of vertex (l & 31) for 16 hands.  It hands those 48 values to
-// its two S waves through LDS; they blend the skinning transforms (DPP row
-// broadcasts, lbs_dpp.h) and write verts while the M wave already runs the
-// next group's MFMAs -- the MFMA pipe and the VALU of every SIMD stay busy at
-// once and v_posed never touches HBM.
+// On gfx950 the f32 MFMA runs on the same datapath as f32 VALU (measured: an
+// f32-MFMA wave and a VALU wave on one SIMD take the SUM of their times, bf16
+// MFMA overlaps), so the fused kernel minimises total ALU work and keeps every
+// product on MFMA, where it runs at full rate:
+//   * the blend GEMM of a 32-hand tile x 32-vertex group: three 32x32 tiles
+//     (x, y, z columns of the same 32 vertices), 73 K-steps each;
+//   * the LBS transforms T_{c,k}[hand][v] = sum_j A_j[c][k] W[v][j]: twelve
+//     32x32 tiles, 8 K-steps (16 joints) each -- 192 MACs per vertex on MFMA
+//     instead of 192 DPP-broadcast VALU FMAs at ~40 % of the VALU peak.
+// Both produce D[hand][v] with the SAME lane layout (lane = vertex, register =
+// hand), so applying T to v_posed is register-local VALU work.  Output rows
+// are staged in LDS and leave as contiguous 12-B (x, y, z) vertex stores: a
+// store of one coordinate at a 12-B stride would be written through as three
+// partial-line writes (measured 3x WRITE_SIZE).  v_posed never touches HBM.
+// T and the apply run in the same operation order as the skin kernel, so the
+// fused and unfused paths agree bit for bit.
 //
-// Barrier-delimited iteration t:  M waves compute tile t (group t/3);  S waves
-// skin group t/3 - 1, in three chunks (one per tile of the current group).
+// Block = 8 waves (2 per SIMD) x 32 hands; the 8 waves share each basis tile
+// (LDS-DMA ring of two), one barrier per tile.
 // ---------------------------------------------------------------------------
 constexpr int kGroupVerts = 32;
-constexpr int kFusedM = 4;                   // M waves per block
-constexpr int kFusedThreads = kFusedM * 3 * 64;
-constexpr int kVpFloats = 3 * 16 * 64;       // one M wave's v_posed hand-off: [q][r/4][lane][4]
-
-__device__ __forceinline__ f32x16 mfma_tile(const float (&a)[kKGroups * 4], const f32x4* __restrict__ b,
-                                            int lane) {
-  f32x16 acc = {};
-  f32x4 bn = b[lane];
-#pragma unroll
-  for (int g = 0; g < kKGroups; ++g) {
-    const f32x4 bv = bn;
-    if (g + 1 < kKGroups) bn = b[(g + 1) * 64 + lane];  // next group's fragments in flight
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (4 * g + q < kKSteps) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * g + q], bv[q], acc, 0, 0, 0);
-  }
-  return acc;
-}
-
-// Block barriers of the fused kernel.  __syncthreads() would also drain every
-// outstanding global store and load (vmcnt(0)) of the S waves at each of the
-// ~78 barriers; only LDS traffic is handed across them.  M waves wait for their
-// LDS-DMA basis staging (vmcnt) and v_posed LDS writes (lgkmcnt); S waves only
-// for their LDS reads.  The "memory" clobber keeps the compiler from moving
-// LDS accesses across.
-__device__ __forceinline__ void barrier_m() {
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-__device__ __forceinline__ void barrier_s() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-__device__ __forceinline__ void put_acc(f32x4* __restrict__ dst, const f32x16& acc, int lane) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) dst[j * 64 + lane] = f32x4{acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]};
-}
+constexpr int kFusedWaves = 8;
+constexpr int kStageFloats = kHandTile * kGroupVerts * 3;  // 3,072 floats = 12 KB per wave
 
 template <bool kTrans>
-__global__ __launch_bounds__(kFusedThreads, 1) void blend_skin_kernel(
+__global__ __launch_bounds__(kFusedWaves * 64, 1) void blend_skin_kernel(
     const float* __restrict__ features, const float* __restrict__ basis_groups,
-    const float* __restrict__ template_groups, const float* __restrict__ weights,
-    const float* __restrict__ transforms, const float* __restrict__ trans,
-    float* __restrict__ verts, float* __restrict__ vposed, int64_t n, int n_verts,
-    int n_groups) {
-  __shared__ f32x4 bs[2][kKGroups * 64];              // basis tile ring      38,912 B
-  __shared__ f32x4 vps[2][kFusedM][kVpFloats / 4];    // v_posed hand-off     98,304 B
-  __shared__ float trs[kFusedM][kHandTile][4];         // translations          2,048 B
+    const float* __restrict__ weight_frags, const float* __restrict__ tfrags,
+    const float* __restrict__ trans, float* __restrict__ verts, float* __restrict__ vposed,
+    int64_t n, int n_verts, int n_groups) {
+  __shared__ f32x4 bs[2][kKGroups * 64];                 // basis tile ring   38,912 B
+  __shared__ float stage[kFusedWaves][kStageFloats];     // output staging    98,304 B
+  __shared__ float trs[kFusedWaves][kHandTile * 3];      // translations       3,072 B
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool is_m = wave < kFusedM;
-  const int mw = is_m ? wave : (wave - kFusedM) >> 1;  // M wave (hand tile) this wave serves
-  const int sh = (wave - kFusedM) & 1;                 // S waves: which half of the 16 rows
+  const int64_t ht = int64_t(blockIdx.x) * kFusedWaves + wave;
   const int64_t n_ht = (n + kHandTile - 1) / kHandTile;
-  const int64_t ht = int64_t(blockIdx.x) * kFusedM + mw;
-  const int64_t h0 = ht * kHandTile;
-  const int n_tiles = 3 * n_groups;
+  const bool active = ht < n_ht;
+  const int64_t htc = active ? ht : n_ht - 1;
   const int hi = lane >> 5;
   const int col = lane & 31;
+  const int64_t h0 = htc * kHandTile;
 
-  // The two roles run separate loops with the same barrier count (n_tiles + 4
-  // s_barrier each), so neither role's registers are live in the other's code.
-  if (is_m) {
-    float a[kKGroups * 4];
-    const int64_t htc = ht < n_ht ? ht : n_ht - 1;
+  float a[kKGroups * 4];
+  {
     const f32x4* src = reinterpret_cast<const f32x4*>(features + htc * kTileFloats) + lane;
 #pragma unroll
     for (int g = 0; g < kKGroups; ++g) {
@@ -351,124 +353,292 @@ __global__ __launch_bounds__(kFusedThreads, 1) void blend_skin_kernel(
       a[4 * g + 2] = v[2];
       a[4 * g + 3] = v[3];
     }
-    stage_basis_tile(basis_groups, 0, bs[0], wave, lane);
-    barrier_m();
-    f32x16 acc0 = {}, acc1 = {};
-    for (int t = 0; t < n_tiles + 3; ++t) {
-      if (t < n_tiles) {
-        if (t + 1 < n_tiles) stage_basis_tile(basis_groups, t + 1, bs[(t + 1) & 1], wave, lane);
-        const f32x4* b = bs[t & 1];
-        const int q = t % 3;
-#ifdef MANO_ABLATE_NO_M  // diagnostic builds only (tools/microbench)
-        if (q == 0) {
-          acc0 = f32x16{};
-        } else if (q == 1) {
-          acc1 = f32x16{};
-        } else {
-          f32x4* dst = vps[(t / 3) & 1][mw];
-          put_acc(dst, acc0, lane);
-          put_acc(dst + 256, acc1, lane);
-          put_acc(dst + 512, acc0, lane);
-        }
-        (void)b;
-#else
-        if (q == 0) {
-          acc0 = mfma_tile(a, b, lane);
-        } else if (q == 1) {
-          acc1 = mfma_tile(a, b, lane);
-        } else {
-          const f32x16 acc2 = mfma_tile(a, b, lane);
-          f32x4* dst = vps[(t / 3) & 1][mw];
-          put_acc(dst, acc0, lane);
-          put_acc(dst + 256, acc1, lane);
-          put_acc(dst + 512, acc2, lane);
-        }
-#endif
-      }
-      barrier_m();
-    }
-    return;
   }
-
-  // ---- S waves ----
-  // S wave `sh` owns MFMA rows r = 8 sh + i (i = 0..7) of its M wave's tile:
-  // row r of lane l is hand h0 + (r & 3) + 8 (r >> 2) + 4 (l >> 5).  The 8 rows'
-  // hands never change, so their 16 joint transforms are loaded ONCE into 96
-  // VGPRs and reused for all vertex groups; per group an S wave only reads the
-  // 24 v_posed values it needs from LDS and streams verts out.
-  const int64_t hmax = n - 1;
-  const int64_t vstride = int64_t(n_verts) * 3;
-  const int64_t hbase = h0 + 16 * sh + 4 * hi;  // row i -> hand hbase + (i & 3) + 8 (i >> 2)
-  float AJ[8][12];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int64_t h = hbase + (i & 3) + 8 * (i >> 2);
-    lbs_load_joint_row(transforms + (h < hmax ? h : hmax) * kTransformFloats, lane, AJ[i]);
-  }
-  if constexpr (kTrans) {  // the tile's 32 translations go to LDS (no VGPRs held)
-    if (sh == 0 && lane < kHandTile) {
+  if constexpr (kTrans) {  // the wave's 32 translations, read back at the stores
+    if (lane < kHandTile) {
       const int64_t h = h0 + lane;
-      const float* tp = trans + (h < hmax ? h : hmax) * 3;
-      trs[mw][lane][0] = tp[0];
-      trs[mw][lane][1] = tp[1];
-      trs[mw][lane][2] = tp[2];
+      const int64_t hc = h < n ? h : n - 1;
+      trs[wave][lane * 3 + 0] = trans[hc * 3 + 0];
+      trs[wave][lane * 3 + 1] = trans[hc * 3 + 1];
+      trs[wave][lane * 3 + 2] = trans[hc * 3 + 2];
     }
   }
-  barrier_s();
-  // Pass grp = -1 only keeps the barrier count equal to the M waves' (n_tiles + 3).
-  for (int grp = -1; grp < n_groups; ++grp) {
+  const f32x4* tf = reinterpret_cast<const f32x4*>(tfrags + htc * kTFragFloats) + lane;
+  const int vstride32 = 3 * n_verts;
+  const int64_t n_left = n - h0;
+  const int n_valid = active ? (n_left < kHandTile ? int(n_left) : kHandTile) : 0;
+  float* vtile = verts + h0 * int64_t(vstride32);
+  float* ptile = vposed ? vposed + h0 * int64_t(vstride32) : nullptr;
+  float* st = stage[wave];
+  const int n_tiles = 3 * n_groups;
+
+  stage_basis_tile<kFusedWaves>(basis_groups, 0, bs[0], wave, lane);
+  __syncthreads();
+
+  for (int grp = 0; grp < n_groups; ++grp) {
+    // The transform fragments are the same for every group; re-read them from
+    // L2 per group rather than pin 96 VGPRs (the empty asm hides the loop
+    // invariance from LICM).
+    int tfo = 0;
+    asm volatile("" : "+s"(tfo));
+    const f32x4* tfg = tf + tfo;
+    // W^T fragments of this vertex group (B operand of the LBS tiles).
+    float wf[8];
+    {
+      const f32x4* wp = reinterpret_cast<const f32x4*>(weight_frags + int64_t(grp) * kWFragFloats) + lane;
+      const f32x4 w0 = wp[0], w1 = wp[64];
+      wf[0] = w0[0]; wf[1] = w0[1]; wf[2] = w0[2]; wf[3] = w0[3];
+      wf[4] = w1[0]; wf[5] = w1[1]; wf[6] = w1[2]; wf[7] = w1[3];
+    }
+    // ---- blend GEMM: v_posed x, y, z of 32 vertices for the 32 hands ----
+    // LBS tile i = (c = i / 4, k = 3 - i % 4) uses fragments F[i & 1][0..1]
+    // (K steps 0-3 and 4-7); tile i+1's are requested while tile i runs, and
+    // tile 0's before the last GEMM tile.
+    f32x4 F[2][2];
+    f32x16 p[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int t = 3 * grp + q;
+      if (t + 1 < n_tiles) stage_basis_tile<kFusedWaves>(basis_groups, t + 1, bs[(t + 1) & 1], wave, lane);
+      if (q == 2) {
+        F[0][0] = tfg[(3 * 2 + 0) * 64];
+        F[0][1] = tfg[(3 * 2 + 1) * 64];
+      }
+      p[q] = mfma_tile(a, bs[t & 1], lane);
+      __syncthreads();
+    }
     int vb = grp * kGroupVerts;
     if (vb > n_verts - kGroupVerts) vb = n_verts - kGroupVerts;
-    const int v = vb + col;
-    float w[kJoints];
-    float tx = 0.f, ty = 0.f, tz = 0.f;
-    if (grp >= 0) {
-      const f32x4* wp = reinterpret_cast<const f32x4*>(weights + int64_t(v) * kJoints);
+    // Store-loop addressing is recomputed per group from a laundered lane id:
+    // hoisted out of the loop, its 32 loop-invariant offsets would spill.
+    int lane_g = lane;
+    asm volatile("" : "+v"(lane_g));
+    if (ptile) {  // rest_verts requested: stage and store v_posed like verts below
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const f32x4 qv = wp[i];
-        w[4 * i + 0] = qv[0];
-        w[4 * i + 1] = qv[1];
-        w[4 * i + 2] = qv[2];
-        w[4 * i + 3] = qv[3];
+      for (int c = 0; c < 3; ++c) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int hr = (r & 3) + 8 * (r >> 2) + 4 * hi;
+          st[hr * (kGroupVerts * 3) + 3 * col + c] = p[c][r];
+        }
       }
-      tx = template_groups[(grp * 3 + 0) * kColTile + col];
-      ty = template_groups[(grp * 3 + 1) * kColTile + col];
-      tz = template_groups[(grp * 3 + 2) * kColTile + col];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const int idx = m * 64 + lane_g;
+        const int hand = idx >> 5, vv = idx & 31;
+        if (hand < n_valid) {
+          const float* sp = st + hand * (kGroupVerts * 3) + 3 * vv;
+          float* o = ptile + unsigned(hand * vstride32 + 3 * (vb + vv));
+          o[0] = sp[0];
+          o[1] = sp[1];
+          o[2] = sp[2];
+        }
+      }
     }
-    const float* vsrc = reinterpret_cast<const float*>(vps[(grp < 0 ? 0 : grp) & 1][mw]);
+    // ---- LBS: out_c = fma(T_c0, x, fma(T_c1, y, fma(T_c2, z, T_c3))) ----
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      if (grp >= 0) {
-        const int li = ((2 * sh + (i >> 2)) * 64 + lane) * 4 + (i & 3);
-        const float p0 = vsrc[li] + tx, p1 = vsrc[1024 + li] + ty, p2 = vsrc[2048 + li] + tz;
-        float T[12];
-        lbs_blend16(T, AJ[i], w);
-        float o0 = fmaf(T[0], p0, fmaf(T[1], p1, fmaf(T[2], p2, T[3])));
-        float o1 = fmaf(T[4], p0, fmaf(T[5], p1, fmaf(T[6], p2, T[7])));
-        float o2 = fmaf(T[8], p0, fmaf(T[9], p1, fmaf(T[10], p2, T[11])));
-        if constexpr (kTrans) {
-          const int hl = 16 * sh + 4 * hi + (i & 3) + 8 * (i >> 2);
-          o0 += trs[mw][hl][0];
-          o1 += trs[mw][hl][1];
-          o2 += trs[mw][hl][2];
+    for (int c = 0; c < 3; ++c) {
+      f32x16 out;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int i = c * 4 + kk;
+        const int k = 3 - kk;  // translation column first, as in the skin kernel
+        if (i + 1 < 12) {
+          const int cn = (i + 1) / 4, kn = 3 - (i + 1) % 4;
+          F[(i + 1) & 1][0] = tfg[((cn * 4 + kn) * 2 + 0) * 64];
+          F[(i + 1) & 1][1] = tfg[((cn * 4 + kn) * 2 + 1) * 64];
         }
-        const int64_t h = hbase + (i & 3) + 8 * (i >> 2);
-        if (h < n) {
-          float* o = verts + h * vstride + 3 * v;
-          o[0] = o0;
-          o[1] = o1;
-          o[2] = o2;
-          if (vposed) {
-            float* pv = vposed + h * vstride + 3 * v;
-            pv[0] = p0;
-            pv[1] = p1;
-            pv[2] = p2;
-          }
+        const f32x4 f0 = F[i & 1][0];
+        const f32x4 f1 = F[i & 1][1];
+        f32x16 T = {};
+        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f0[0], wf[0], T, 0, 0, 0);
+        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f0[1], wf[1], T, 0, 0, 0);
+        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f0[2], wf[2], T, 0, 0, 0);
+        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f0[3], wf[3], T, 0, 0, 0);
+        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f1[0], wf[4], T, 0, 0, 0);
+        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f1[1], wf[5], T, 0, 0, 0);
+        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f1[2], wf[6], T, 0, 0, 0);
+        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f1[3], wf[7], T, 0, 0, 0);
+        if (k == 3) {
+          out = T;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) out[r] = fmaf(T[r], p[k][r], out[r]);
         }
       }
-      // three barriers per group, after rows 2, 5 and 7 (one per M-wave tile)
-      if (i == 2 || i == 5 || i == 7) barrier_s();
+      // stage component c: row = hand (register r), 3 floats per vertex (lane)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int hr = (r & 3) + 8 * (r >> 2) + 4 * hi;
+        float o = out[r];
+        if constexpr (kTrans) o += trs[wave][hr * 3 + c];
+        st[hr * (kGroupVerts * 3) + 3 * col + c] = o;
+      }
+    }
+    // ---- contiguous stores: 16 (hand, vertex) points per lane, 12 B each ----
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      if ((m & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+      const int idx = m * 64 + lane_g;
+      const int hand = idx >> 5, vv = idx & 31;
+      if (hand < n_valid) {
+        const float* sp = st + hand * (kGroupVerts * 3) + 3 * vv;
+        float* o = vtile + unsigned(hand * vstride32 + 3 * (vb + vv));
+        o[0] = sp[0];
+        o[1] = sp[1];
+        o[2] = sp[2];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// blend_skin, register-resident form: 4 waves per block, one wave per SIMD and
+// the whole 512-entry register file per wave -- the 32 hands' transform
+// fragments stay in VGPRs for all vertex groups, the three output components
+// of a vertex are in registers together, so each lane stores contiguous 12-B
+// (x, y, z) points straight to HBM with no LDS staging.
+// ---------------------------------------------------------------------------
+template <bool kTrans>
+__global__ __launch_bounds__(256, 1) void blend_skin_reg_kernel(
+    const float* __restrict__ features, const float* __restrict__ basis_groups,
+    const float* __restrict__ weight_frags, const float* __restrict__ tfrags,
+    const float* __restrict__ trans, float* __restrict__ verts, float* __restrict__ vposed,
+    int64_t n, int n_verts, int n_groups) {
+  __shared__ f32x4 bs[2][kKGroups * 64];
+  __shared__ float trs[4][kHandTile * 3];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t ht = int64_t(blockIdx.x) * 4 + wave;
+  const int64_t n_ht = (n + kHandTile - 1) / kHandTile;
+  const bool active = ht < n_ht;
+  const int64_t htc = active ? ht : n_ht - 1;
+  const int hi = lane >> 5;
+  const int col = lane & 31;
+  const int64_t h0 = htc * kHandTile;
+
+  float a[kKGroups * 4];
+  {
+    const f32x4* src = reinterpret_cast<const f32x4*>(features + htc * kTileFloats) + lane;
+#pragma unroll
+    for (int g = 0; g < kKGroups; ++g) {
+      const f32x4 v = src[g * 64];
+      a[4 * g + 0] = v[0];
+      a[4 * g + 1] = v[1];
+      a[4 * g + 2] = v[2];
+      a[4 * g + 3] = v[3];
+    }
+  }
+  if constexpr (kTrans) {
+    if (lane < kHandTile) {
+      const int64_t h = h0 + lane;
+      const int64_t hc = h < n ? h : n - 1;
+      trs[wave][lane * 3 + 0] = trans[hc * 3 + 0];
+      trs[wave][lane * 3 + 1] = trans[hc * 3 + 1];
+      trs[wave][lane * 3 + 2] = trans[hc * 3 + 2];
+    }
+  }
+  const f32x4* tf = reinterpret_cast<const f32x4*>(tfrags + htc * kTFragFloats) + lane;
+  const int vstride32 = 3 * n_verts;
+  const int64_t n_left = n - h0;
+  const int n_valid = active ? (n_left < kHandTile ? int(n_left) : kHandTile) : 0;
+  float* vtile = verts + h0 * int64_t(vstride32);
+  float* ptile = vposed ? vposed + h0 * int64_t(vstride32) : nullptr;
+  const int n_tiles = 3 * n_groups;
+
+  stage_basis_tile(basis_groups, 0, bs[0], wave, lane);
+  __syncthreads();
+
+  for (int grp = 0; grp < n_groups; ++grp) {
+    // Transform fragments (the same for every group) stream from L2 one LBS
+    // tile ahead; the empty asm keeps LICM from pinning all 96 VGPRs of them.
+    int tfo = 0;
+    asm volatile("" : "+s"(tfo));
+    const f32x4* tfg = tf + tfo;
+    float wf[8];
+    {
+      const f32x4* wp = reinterpret_cast<const f32x4*>(weight_frags + int64_t(grp) * kWFragFloats) + lane;
+      const f32x4 w0 = wp[0], w1 = wp[64];
+      wf[0] = w0[0]; wf[1] = w0[1]; wf[2] = w0[2]; wf[3] = w0[3];
+      wf[4] = w1[0]; wf[5] = w1[1]; wf[6] = w1[2]; wf[7] = w1[3];
+    }
+    f32x4 F[2][2];
+    f32x16 p[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int t = 3 * grp + q;
+      if (t + 1 < n_tiles) stage_basis_tile(basis_groups, t + 1, bs[(t + 1) & 1], wave, lane);
+      if (q == 2) {  // LBS tile 0 = (c 0, k 3)
+        F[0][0] = tfg[(3 * 2 + 0) * 64];
+        F[0][1] = tfg[(3 * 2 + 1) * 64];
+      }
+      p[q] = mfma_tile(a, bs[t & 1], lane);
+      __syncthreads();
+    }
+    int vb = grp * kGroupVerts;
+    if (vb > n_verts - kGroupVerts) vb = n_verts - kGroupVerts;
+    const int voff = 3 * (vb + col);
+    if (ptile) {  // rest_verts requested: store v_posed before p starts dying
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int hr = (r & 3) + 8 * (r >> 2) + 4 * hi;
+        if (hr < n_valid) {
+          float* pv = ptile + unsigned(hr * vstride32 + voff);
+          pv[0] = p[0][r];
+          pv[1] = p[1][r];
+          pv[2] = p[2][r];
+        }
+      }
+    }
+    f32x16 out[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int i = c * 4 + kk;
+        const int k = 3 - kk;  // translation column first, as in the skin kernel
+        if (i + 1 < 12) {
+          const int cn = (i + 1) / 4, kn = 3 - (i + 1) % 4;
+          F[(i + 1) & 1][0] = tfg[((cn * 4 + kn) * 2 + 0) * 64];
+          F[(i + 1) & 1][1] = tfg[((cn * 4 + kn) * 2 + 1) * 64];
+        }
+        const f32x4 f0 = F[i & 1][0];
+        const f32x4 f1 = F[i & 1][1];
+        f32x16 T = {};
+        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f0[0], wf[0], T, 0, 0, 0);
+        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f0[1], wf[1], T, 0, 0, 0);
+        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f0[2], wf[2], T, 0, 0, 0);
+        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f0[3], wf[3], T, 0, 0, 0);
+        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f1[0], wf[4], T, 0, 0, 0);
+        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f1[1], wf[5], T, 0, 0, 0);
+        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f1[2], wf[6], T, 0, 0, 0);
+        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f1[3], wf[7], T, 0, 0, 0);
+        if (k == 3) {
+          out[c] = T;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) out[c][r] = fmaf(T[r], p[k][r], out[c][r]);
+        }
+        // One LBS tile in flight at a time: left alone, the scheduler issues
+        // all twelve 8-MFMA chains first and keeps 192 VGPRs of results live.
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int hr = (r & 3) + 8 * (r >> 2) + 4 * hi;
+      if (hr < n_valid) {
+        float o0 = out[0][r], o1 = out[1][r], o2 = out[2][r];
+        if constexpr (kTrans) {
+          o0 += trs[wave][hr * 3 + 0];
+          o1 += trs[wave][hr * 3 + 1];
+          o2 += trs[wave][hr * 3 + 2];
+        }
+        float* o = vtile + unsigned(hr * vstride32 + voff);
+        o[0] = o0;
+        o[1] = o1;
+        o[2] = o2;
+      }
     }
   }
 }
@@ -586,12 +756,13 @@ __global__ __launch_bounds__(256) void rodrigues_kernel(const float* __restrict_
 
 hipError_t launch_articulate(const DeviceModel& m, int64_t n, const float* betas,
                              int64_t betas_stride, const float* pose, const float* trans,
-                             float* features, float* transforms, float* joints,
+                             float* features, float* transforms, float* tfrags, float* joints,
                              float* rest_joints, float* rot_mats, hipStream_t stream) {
   const int64_t blocks = (n + kHandTile - 1) / kHandTile;
   hipLaunchKernelGGL(articulate_kernel, dim3(unsigned(blocks)), dim3(512), 0, stream, betas,
                      betas_stride, pose, trans, m.joint_template, m.joint_shape, m.parents,
-                     m.depth, m.max_depth, n, features, transforms, joints, rest_joints, rot_mats);
+                     m.depth, m.max_depth, n, features, transforms, tfrags, joints, rest_joints,
+                     rot_mats);
   return hipGetLastError();
 }
 
@@ -600,23 +771,39 @@ hipError_t launch_blend(const DeviceModel& m, int64_t n, const float* features, 
   const int64_t n_ht = (n + kHandTile - 1) / kHandTile;
   const int64_t blocks = (n_ht + 3) / 4;
   hipLaunchKernelGGL(blend_kernel, dim3(unsigned(blocks)), dim3(256), 0, stream, features,
-                     m.basis_tiles, m.template_cols, vposed, n, m.n_cols, m.n_col_tiles);
+                     m.basis_tiles, vposed, n, m.n_cols, m.n_col_tiles);
   return hipGetLastError();
 }
 
+#ifndef MANO_FUSED_IMPL
+#define MANO_FUSED_IMPL 1  // 0: 8-wave LDS-staged form, 1: register-resident form
+#endif
+
 hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features,
-                             const float* transforms, const float* trans, float* verts,
+                             const float* tfrags, const float* trans, float* verts,
                              float* vposed, hipStream_t stream) {
   const int64_t n_ht = (n + kHandTile - 1) / kHandTile;
-  const int64_t blocks = (n_ht + kFusedM - 1) / kFusedM;
+#if MANO_FUSED_IMPL == 0
+  const int64_t blocks = (n_ht + kFusedWaves - 1) / kFusedWaves;
+  const dim3 grid{unsigned(blocks)}, block{unsigned(kFusedWaves * 64)};
   if (trans)
-    hipLaunchKernelGGL(blend_skin_kernel<true>, dim3(unsigned(blocks)), dim3(kFusedThreads), 0,
-                       stream, features, m.basis_groups, m.template_groups, m.weights, transforms,
-                       trans, verts, vposed, n, m.n_verts, m.n_groups);
+    hipLaunchKernelGGL(blend_skin_kernel<true>, grid, block, 0, stream, features, m.basis_groups,
+                       m.weight_frags, tfrags, trans, verts, vposed, n, m.n_verts, m.n_groups);
   else
-    hipLaunchKernelGGL(blend_skin_kernel<false>, dim3(unsigned(blocks)), dim3(kFusedThreads), 0,
-                       stream, features, m.basis_groups, m.template_groups, m.weights, transforms,
-                       trans, verts, vposed, n, m.n_verts, m.n_groups);
+    hipLaunchKernelGGL(blend_skin_kernel<false>, grid, block, 0, stream, features, m.basis_groups,
+                       m.weight_frags, tfrags, trans, verts, vposed, n, m.n_verts, m.n_groups);
+#else
+  const int64_t blocks = (n_ht + 3) / 4;
+  const dim3 grid{unsigned(blocks)}, block{256u};
+  if (trans)
+    hipLaunchKernelGGL(blend_skin_reg_kernel<true>, grid, block, 0, stream, features,
+                       m.basis_groups, m.weight_frags, tfrags, trans, verts, vposed, n, m.n_verts,
+                       m.n_groups);
+  else
+    hipLaunchKernelGGL(blend_skin_reg_kernel<false>, grid, block, 0, stream, features,
+                       m.basis_groups, m.weight_frags, tfrags, trans, verts, vposed, n, m.n_verts,
+                       m.n_groups);
+#endif
   return hipGetLastError();
 }
 

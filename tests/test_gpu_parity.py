@@ -190,7 +190,7 @@ def test_stage_intermediates(engine, dev, params):
     assert np.abs(X[:, :10] - betas).max() < 1e-6
     feats = mano_oracle.pose_features(ref["rot"])
     assert np.abs(X[:, 10:145] - feats).max() <= TOL_R
-    assert np.all(X[:, 145:] == 0.0)
+    assert np.all(X[:, 145] == 1.0) and np.all(X[:, 146:] == 0.0)
     # transforms: oracle G after rest removal, rows 0..2
     _, G = mano_oracle.chain(ref["rot"], ref["rest_joints"], params["parents"])
     assert np.abs(host(inter["transforms"]) - G[:, :, :3, :]).max() <= TOL_M

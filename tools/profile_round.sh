@@ -1,0 +1,27 @@
+#!/bin/bash
+# rocprofv3 evidence for one round: kernel-trace stats of the default bench and
+# separate PMC passes (FETCH_SIZE / WRITE_SIZE / SQ) of the fused and unfused paths.
+# Usage: bash tools/profile_round.sh r01
+set -u
+TAG=${1:-r01}
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+run() {  # name timeout args...
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  if [ $rc -ne 0 ]; then tail -5 "$OUT/$name.log"; exit $rc; fi
+}
+run stats 300 rocprofv3 --kernel-trace --stats -d $OUT/stats -o bench --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu
+cp $OUT/stats.log $OUT/bench_stats_run.log
+for path in fused unfused; do
+  run fetch_$path 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch_$path -o p --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu --path $path
+  run write_$path 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write_$path -o p --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu --path $path
+  run sq_$path 300 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_COEXEC_CYCLES SQ_WAVE_CYCLES -d $OUT/sq_$path -o p --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu --path $path
+  run l2_$path 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT TCC_HIT_sum TCC_MISS_sum -d $OUT/l2_$path -o p --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu --path $path
+done
+python tools/summarize_pmc.py $OUT > $OUT/summary.txt 2>&1; echo summarize rc=$?
+cat $OUT/summary.txt | head -60

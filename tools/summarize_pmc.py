@@ -1,0 +1,53 @@
+"""Summarise a tools/profile_round.sh directory into per-kernel averages.
+
+HBM traffic per launch follows /opt/skills/guides/MI355X_MICROARCH.md §HBM:
+FETCH_SIZE (KB) reads exactly half the bytes of a wide coalesced stream on
+gfx950, so hbm_read = 2 * FETCH_SIZE * 1024 (an upper estimate for narrower
+accesses); hbm_write = WRITE_SIZE * 1024.  Writes `pmc_traffic.json`-style
+JSON on stdout's last line and a readable table before it.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+KERNELS = {"blend_skin_kernel": "blend_skin", "blend_kernel": "blend", "skin_kernel": "skin",
+           "articulate_kernel": "articulate"}
+
+
+def short(name):
+    for k, v in KERNELS.items():
+        if k + "<" in name or k + "(" in name:
+            return v
+    return None
+
+
+def main(d):
+    acc = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(os.path.join(d, "*", "*counter_collection.csv")):
+        path = os.path.basename(os.path.dirname(f)).split("_")[-1]
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            if k is None:
+                continue
+            acc[(k, path)][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    out = {"batch": 65536, "kernels": {}}
+    for (k, path), cs in sorted(acc.items()):
+        avg = {c: sum(v) / len(v) for c, v in cs.items()}
+        print(f"{k:12s} [{path}]")
+        for c, v in sorted(avg.items()):
+            print(f"    {c:32s} {v:.6g}")
+        if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+            rd = 2 * avg["FETCH_SIZE"] * 1024
+            wr = avg["WRITE_SIZE"] * 1024
+            print(f"    -> hbm read {rd/1e6:.1f} MB (2x FETCH_SIZE), write {wr/1e6:.1f} MB per launch")
+            out["kernels"][k] = {"hbm_bytes_per_launch": rd + wr, "hbm_read_bytes": rd,
+                                 "hbm_write_bytes": wr, "fetch_size_kb": avg["FETCH_SIZE"],
+                                 "write_size_kb": avg["WRITE_SIZE"], "path": path}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
