@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="process-group backend for N > 1 (gloo: CPU rehearsal, ranks may share a GPU)")
     return ap.parse_args()
 
 
@@ -90,10 +92,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # One process per GPU.  `--backend gloo` is a control-flow rehearsal mode
+    # (several ranks may share one GPU); the real multi-GPU run uses RCCL.
+    ndev = torch.cuda.device_count()
+    local_dev = local if args.backend == "nccl" else local % max(ndev, 1)
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from mano_amd import ManoHip, load_dump, synthetic_params
     from mano_amd.distributed import gather_to_root
@@ -130,8 +139,11 @@ def main():
             if evs is not None:
                 evs[3].record(stream)
         if args.gather and world > 1:
-            gather_to_root(verts, B * world, root=0)
-            gather_to_root(joints, B * world, root=0)
+            if args.backend == "nccl":  # RCCL over xGMI, device to device
+                gather_to_root(verts, B * world, root=0)
+                gather_to_root(joints, B * world, root=0)
+            else:
+                gather_to_root(joints.cpu(), B * world, root=0)
 
     for _ in range(args.warmup):
         step()
@@ -149,7 +161,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt], device=dev if args.backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 

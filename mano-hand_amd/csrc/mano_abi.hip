@@ -203,6 +203,33 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
               float(skinning_weights[size_t(v) * kJoints + jj]);
       }
   }
+  // 16x16x4 fused layout: group g = 16 vertices from min(16g, V-16).
+  const int n_groups16 = (V + 15) / 16;
+  std::vector<float> b16(size_t(n_groups16) * 3 * kTile16Floats, 0.f);
+  std::vector<float> w16(size_t(n_groups16) * kWFrag16Floats, 0.f);
+  for (int g = 0; g < n_groups16; ++g) {
+    const int vb = std::max(0, std::min(16 * g, V - 16));
+    for (int l = 0; l < 64; ++l) {
+      const int v = vb + (l & 15);
+      for (int st = 0; st < 4; ++st)
+        if (v < V)
+          w16[size_t(g) * kWFrag16Floats + l * 4 + st] =
+              float(skinning_weights[size_t(v) * kJoints + 4 * st + (l >> 4)]);
+      for (int q = 0; q < 3; ++q)
+        for (int gg = 0; gg < kGroups16; ++gg)
+          for (int qq = 0; qq < 4; ++qq) {
+            const int k = 4 * (4 * gg + qq) + (l >> 4);
+            float val = 0.f;
+            if (k <= kK && v < V) {
+              const size_t colv = size_t(v) * 3 + q;
+              val = k < kShape ? float(mesh_shape_basis[colv * kShape + k])
+                    : k < kK   ? float(mesh_pose_basis[colv * kPoseFeats + (k - kShape)])
+                               : float(mesh_template[colv]);
+            }
+            b16[((size_t(g) * 3 + q) * kGroups16 + gg) * 256 + l * 4 + qq] = val;
+          }
+    }
+  }
   std::vector<float> tmpl(size_t(n_col_tiles) * kColTile, 0.f);
   for (int i = 0; i < n_cols; ++i) tmpl[i] = float(mesh_template[i]);
   std::vector<float> wts(size_t(V) * kJoints);
@@ -222,7 +249,8 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
       {depth.data(), kJoints * 4, 0},      {pca.data(), pca.size() * 4, 0},
       {pmean.data(), pmean.size() * 4, 0}, {zeros.data(), zeros.size() * 4, 0},
       {gtiles.data(), gtiles.size() * 4, 0}, {gtmpl.data(), gtmpl.size() * 4, 0},
-      {wfr.data(), wfr.size() * 4, 0}};
+      {wfr.data(), wfr.size() * 4, 0}, {b16.data(), b16.size() * 4, 0},
+      {w16.data(), w16.size() * 4, 0}};
   size_t total = 0;
   for (auto& p : parts) {
     p.off = total;
@@ -261,6 +289,9 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   m->dm.template_groups = reinterpret_cast<float*>(b + parts[11].off);
   m->dm.weight_frags = reinterpret_cast<float*>(b + parts[12].off);
   m->dm.n_groups = n_groups;
+  m->dm.basis16 = reinterpret_cast<float*>(b + parts[13].off);
+  m->dm.wfrag16 = reinterpret_cast<float*>(b + parts[14].off);
+  m->dm.n_groups16 = n_groups16;
   m->dm.max_depth = max_depth;
   m->dm.n_verts = V;
   m->dm.n_cols = n_cols;
@@ -327,7 +358,9 @@ int mano_stage_articulate(const mano_model* m, int64_t n, const float* betas,
   hipError_t e = mano::launch_articulate(
       m->dm, n, betas, betas_stride, pose, trans, reinterpret_cast<float*>(base + w.features_off),
       reinterpret_cast<float*>(base + w.transforms_off),
-      reinterpret_cast<float*>(base + w.tfrag_off), joints, rest_joints, rot_mats,
+      reinterpret_cast<float*>(base + w.tfrag_off),
+      reinterpret_cast<float*>(base + w.features16_off),
+      reinterpret_cast<float*>(base + w.tfrag16_off), joints, rest_joints, rot_mats,
       static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "articulate launch");
   return MANO_OK;
@@ -382,7 +415,9 @@ int mano_stage_blend_skin(const mano_model* m, int64_t n, float* rest_verts, con
   char* base = static_cast<char*>(ws);
   hipError_t e = mano::launch_blend_skin(
       m->dm, n, reinterpret_cast<const float*>(base + w.features_off),
-      reinterpret_cast<const float*>(base + w.tfrag_off), trans, verts, rest_verts,
+      reinterpret_cast<const float*>(base + w.tfrag_off),
+      reinterpret_cast<const float*>(base + w.features16_off),
+      reinterpret_cast<const float*>(base + w.tfrag16_off), trans, verts, rest_verts,
       static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "blend_skin launch");
   return MANO_OK;

@@ -29,6 +29,18 @@ constexpr int kTransformFloats = kJoints * 12; // 3x4 skinning transform per joi
 //   W fragments, per vertex group: [s/4][lane][s%4]     = W[vb + (lane&31)][2s + (lane>>5)]
 constexpr int kTFragFloats = 12 * 8 * 64;      // 6144 floats = 24 KB per hand tile
 constexpr int kWFragFloats = 8 * 64;           // 512 floats per vertex group
+// 16x16x4 form of the fused kernel (16-hand tiles, 16-vertex groups):
+//   features16 per 16 hands: [10][64][4], lane l, step s = 4g + q:
+//       X[16 t + (l & 15)][k = 4 s + (l >> 4)]            (K padded to 160)
+//   basis16 per vertex group (3 tiles x, y, z): [10][64][4]:
+//       B[k = 4 s + (l >> 4)][3 (vb + (l & 15)) + coord]
+//   tfrag16 per 16 hands: [12 (c*4+k)][64][4]: A_{4 s + (l >> 4)}(16 t + (l & 15))[c][k]
+//   wfrag16 per vertex group: [64][4]: W[vb + (l & 15)][4 s + (l >> 4)]
+constexpr int kSteps16 = (kK + 1 + 3) / 4;     // 37 MFMA steps (K = 146 -> 148)
+constexpr int kGroups16 = (kSteps16 + 3) / 4;  // 10 float4 groups per lane
+constexpr int kTile16Floats = kGroups16 * 64 * 4;   // 2560 floats = 10 KB
+constexpr int kTFrag16Floats = 12 * 64 * 4;    // 3072 floats = 12 KB per 16 hands
+constexpr int kWFrag16Floats = 64 * 4;         // 256 floats per 16-vertex group
 
 // Device-resident model buffer (float32, layouts chosen for the kernels).
 struct DeviceModel {
@@ -45,16 +57,19 @@ struct DeviceModel {
   float* basis_groups;  // [n_groups][3][kKGroups][64][4] B tiles: x|y|z of 32 verts
   float* template_groups; // [n_groups][3][32] template coordinate per group column
   float* weight_frags;  // [n_groups][kWFragFloats] MFMA B fragments of W^T per group
+  float* basis16;       // [n_groups16][3][kTile16Floats]
+  float* wfrag16;       // [n_groups16][kWFrag16Floats]
   int32_t max_depth;
   int32_t n_verts;
   int32_t n_cols;       // 3V
   int32_t n_col_tiles;  // ceil(3V / 32)
   int32_t n_groups;     // ceil(V / 32) vertex groups of the fused kernel (last one shifted)
+  int32_t n_groups16;   // ceil(V / 16) groups of the 16x16 fused kernel (last one shifted)
 };
 
 // Workspace carving (all offsets 256-B aligned).
 struct Workspace {
-  size_t features_off, transforms_off, tfrag_off, vposed_off, total;
+  size_t features_off, transforms_off, tfrag_off, features16_off, tfrag16_off, vposed_off, total;
 };
 
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -65,7 +80,9 @@ inline Workspace workspace_layout(const DeviceModel& m, int64_t n) {
   w.features_off = 0;
   w.transforms_off = align256(w.features_off + size_t(n_tiles) * kTileFloats * sizeof(float));
   w.tfrag_off = align256(w.transforms_off + size_t(n) * kTransformFloats * sizeof(float));
-  w.vposed_off = align256(w.tfrag_off + size_t(n_tiles) * kTFragFloats * sizeof(float));
+  w.features16_off = align256(w.tfrag_off + size_t(n_tiles) * kTFragFloats * sizeof(float));
+  w.tfrag16_off = align256(w.features16_off + size_t(2 * n_tiles) * kTile16Floats * sizeof(float));
+  w.vposed_off = align256(w.tfrag16_off + size_t(2 * n_tiles) * kTFrag16Floats * sizeof(float));
   w.total = align256(w.vposed_off + size_t(n) * m.n_cols * sizeof(float));
   return w;
 }
@@ -73,13 +90,14 @@ inline Workspace workspace_layout(const DeviceModel& m, int64_t n) {
 // Kernel launchers (mano_kernels.hip).  All asynchronous on `stream`.
 hipError_t launch_articulate(const DeviceModel& m, int64_t n, const float* betas,
                              int64_t betas_stride, const float* pose, const float* trans,
-                             float* features, float* transforms, float* tfrags, float* joints,
+                             float* features, float* transforms, float* tfrags,
+                             float* features16, float* tfrag16, float* joints,
                              float* rest_joints, float* rot_mats, hipStream_t stream);
 hipError_t launch_blend(const DeviceModel& m, int64_t n, const float* features,
                         float* vposed, hipStream_t stream);
 hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features,
-                             const float* tfrags, const float* trans, float* verts,
-                             float* vposed, hipStream_t stream);
+                             const float* tfrags, const float* features16, const float* tfrag16,
+                             const float* trans, float* verts, float* vposed, hipStream_t stream);
 hipError_t launch_skin(const DeviceModel& m, int64_t n, const float* transforms,
                        const float* vposed, const float* trans, float* verts,
                        hipStream_t stream);

@@ -68,11 +68,16 @@ __global__ __launch_bounds__(512) void articulate_kernel(
     const float* __restrict__ joint_shape, const int32_t* __restrict__ parents,
     const int32_t* __restrict__ depth, int max_depth, int64_t n,
     float* __restrict__ features, float* __restrict__ transforms, float* __restrict__ tfrags,
-    float* __restrict__ joints, float* __restrict__ rest_joints, float* __restrict__ rot_mats) {
+    float* __restrict__ features16, float* __restrict__ tfrag16, float* __restrict__ joints,
+    float* __restrict__ rest_joints, float* __restrict__ rot_mats) {
   __shared__ f32x4 tile[kKGroups * 64];
   __shared__ f32x4 ttile[kTFragFloats / 4];
+  __shared__ f32x4 tile16[2 * kTile16Floats / 4];
+  __shared__ f32x4 ttile16[2 * kTFrag16Floats / 4];
   float* tilef = reinterpret_cast<float*>(tile);
   float* ttilef = reinterpret_cast<float*>(ttile);
+  float* tile16f = reinterpret_cast<float*>(tile16);
+  float* ttile16f = reinterpret_cast<float*>(ttile16);
 
   const int tid = threadIdx.x;
   const int j = tid & (kJoints - 1);
@@ -157,6 +162,11 @@ __global__ __launch_bounds__(512) void articulate_kernel(
     const int ln = hl + 32 * (j & 1);
 #pragma unroll
     for (int ck = 0; ck < 12; ++ck) ttilef[((ck * 2 + (s >> 2)) * 64 + ln) * 4 + (s & 3)] = Aj[ck];
+    // 16x16x4 layout: hand (hl & 15) of 16-hand tile (hl >> 4), joint j = 4 s16 + (l >> 4)
+    const int ln16 = (hl & 15) + 16 * (j & 3);
+    float* t16 = ttile16f + (hl >> 4) * kTFrag16Floats;
+#pragma unroll
+    for (int ck = 0; ck < 12; ++ck) t16[(ck * 64 + ln16) * 4 + (j >> 2)] = Aj[ck];
   }
   if (valid) {
     float* A = transforms + h * kTransformFloats + j * 12;
@@ -184,17 +194,22 @@ __global__ __launch_bounds__(512) void articulate_kernel(
   // (selects the template row of the basis), zeros up to 152.
   // Fragment layout for v_mfma_f32_32x32x2_f32: step s = k/2 holds
   // X[hand = lane & 31][k = 2s + (lane >> 5)]; 4 steps packed per float4.
+  float* t16 = tile16f + (hl >> 4) * kTile16Floats;
   auto put = [&](int k, float v) {
     const int s = k >> 1;
     const int ln = hl + 32 * (k & 1);
-    tilef[(((s >> 2) * 64) + ln) * 4 + (s & 3)] = v;
+    if (k < kKGroups * 8) tilef[(((s >> 2) * 64) + ln) * 4 + (s & 3)] = v;
+    if (k < kGroups16 * 16) {  // 16x16x4 fragments: step s16 = k / 4, lane (hl & 15) + 16 (k & 3)
+      const int s16 = k >> 2;
+      t16[(((s16 >> 2) * 64) + (hl & 15) + 16 * (k & 3)) * 4 + (s16 & 3)] = v;
+    }
   };
   if (j == 0) {
 #pragma unroll
     for (int s = 0; s < kShape; ++s) put(s, beta[s]);
     put(kK, 1.f);  // X[:, 145] = 1 multiplies the template row of the basis
 #pragma unroll
-    for (int k = kK + 1; k < kKGroups * 8; ++k) put(k, 0.f);
+    for (int k = kK + 1; k < kGroups16 * 16; ++k) put(k, 0.f);
   } else {
 #pragma unroll
     for (int m = 0; m < 9; ++m) put(kShape + 9 * (j - 1) + m, rm[m]);
@@ -204,6 +219,10 @@ __global__ __launch_bounds__(512) void articulate_kernel(
   for (int i = tid; i < kKGroups * 64; i += 512) dst[i] = tile[i];
   f32x4* tdst = reinterpret_cast<f32x4*>(tfrags + int64_t(blockIdx.x) * kTFragFloats);
   for (int i = tid; i < kTFragFloats / 4; i += 512) tdst[i] = ttile[i];
+  f32x4* d16 = reinterpret_cast<f32x4*>(features16 + int64_t(blockIdx.x) * 2 * kTile16Floats);
+  for (int i = tid; i < 2 * kTile16Floats / 4; i += 512) d16[i] = tile16[i];
+  f32x4* t16d = reinterpret_cast<f32x4*>(tfrag16 + int64_t(blockIdx.x) * 2 * kTFrag16Floats);
+  for (int i = tid; i < 2 * kTFrag16Floats / 4; i += 512) t16d[i] = ttile16[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -250,6 +269,16 @@ __device__ __forceinline__ void store_vposed_tile(float* __restrict__ vposed, co
       const int64_t h = h0 + (r & 3) + 8 * (r >> 2) + 4 * hi;
       if (h < n) vposed[h * n_cols + col] = acc[r];
     }
+  }
+}
+
+__device__ __forceinline__ void stage_basis_tile16(const float* __restrict__ basis16, int t,
+                                                   f32x4* buf, int wave, int lane) {
+  const float* src = basis16 + int64_t(t) * kTile16Floats + lane * 4;
+  for (int g = wave; g < kGroups16; g += 4) {
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)(src + g * 256),
+        (__attribute__((address_space(3))) void*)(buf + g * 64), 16, 0, 0);
   }
 }
 
@@ -644,6 +673,143 @@ __global__ __launch_bounds__(256, 1) void blend_skin_reg_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// blend_skin16: the fused kernel on v_mfma_f32_16x16x4_f32 (16-hand tiles,
+// 16-vertex groups).  Same algorithm as blend_skin (GEMM tiles x, y, z of a
+// vertex group + 12 LBS transform tiles, register-local apply), but a wave
+// needs ~half the registers (37 A-fragment VGPRs, 4-register accumulators),
+// so the transform fragments stay resident and 3 waves share each SIMD --
+// enough to cover the 40-cycle dependent latency of the 16x16x4 chains and
+// each other's barrier / LDS / store stalls.
+// ---------------------------------------------------------------------------
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma16_tile(const float (&a)[kGroups16 * 4],
+                                             const f32x4* __restrict__ b, int lane) {
+  f32x4 acc = {};
+  f32x4 bn = b[lane];
+#pragma unroll
+  for (int g = 0; g < kGroups16; ++g) {
+    const f32x4 bv = bn;
+    if (g + 1 < kGroups16) bn = b[(g + 1) * 64 + lane];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (4 * g + q < kSteps16) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[4 * g + q], bv[q], acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+template <bool kTrans>
+__global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
+    const float* __restrict__ features16, const float* __restrict__ basis16,
+    const float* __restrict__ wfrag16, const float* __restrict__ tfrag16,
+    const float* __restrict__ trans, float* __restrict__ verts, float* __restrict__ vposed,
+    int64_t n, int n_verts, int n_groups) {
+  __shared__ f32x4 bs[2][kGroups16 * 64];  // basis tile ring 2 x 10 KB
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nt16 = (n + 15) / 16;
+  const int64_t t16 = int64_t(blockIdx.x) * 4 + wave;
+  const bool active = t16 < nt16;
+  const int64_t tc = active ? t16 : nt16 - 1;
+  const int64_t h0 = tc * 16;
+  const int row0 = 4 * (lane >> 4);  // D rows (hands) of this lane: row0 + r
+  const int col = lane & 15;         // D column (vertex of the group)
+
+  float a[kGroups16 * 4];
+  {
+    const f32x4* src = reinterpret_cast<const f32x4*>(features16 + tc * kTile16Floats) + lane;
+#pragma unroll
+    for (int g = 0; g < kGroups16; ++g) {
+      const f32x4 v = src[g * 64];
+      a[4 * g + 0] = v[0];
+      a[4 * g + 1] = v[1];
+      a[4 * g + 2] = v[2];
+      a[4 * g + 3] = v[3];
+    }
+  }
+  f32x4 F[12];  // LBS A fragments, tile (c, k) = c * 4 + k, resident for all groups
+  {
+    const f32x4* src = reinterpret_cast<const f32x4*>(tfrag16 + tc * kTFrag16Floats) + lane;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) F[i] = src[i * 64];
+  }
+  __shared__ float trs[4][16 * 3];  // the wave's 16 translations, read back at the stores
+  if constexpr (kTrans) {
+    if (lane < 48) {
+      const int64_t h = h0 + lane / 3;
+      trs[wave][lane] = trans[(h < n ? h : n - 1) * 3 + lane % 3];
+    }
+  }
+  const int vstride32 = 3 * n_verts;
+  const int64_t n_left = n - h0;
+  const int n_valid = active ? (n_left < 16 ? int(n_left) : 16) : 0;
+  float* vtile = verts + h0 * int64_t(vstride32);
+  float* ptile = vposed ? vposed + h0 * int64_t(vstride32) : nullptr;
+  const int n_tiles = 3 * n_groups;
+
+  stage_basis_tile16(basis16, 0, bs[0], wave, lane);
+  __syncthreads();
+
+  for (int grp = 0; grp < n_groups; ++grp) {
+    const f32x4 wf = reinterpret_cast<const f32x4*>(wfrag16 + int64_t(grp) * kWFrag16Floats)[lane];
+    f32x4 p[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int t = 3 * grp + q;
+      if (t + 1 < n_tiles) stage_basis_tile16(basis16, t + 1, bs[(t + 1) & 1], wave, lane);
+      p[q] = mfma16_tile(a, bs[t & 1], lane);
+      __syncthreads();
+    }
+    int vb = grp * 16;
+    if (vb > n_verts - 16) vb = n_verts - 16;
+    const int voff = 3 * (vb + col);
+    f32x4 out[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int k = 3 - kk;  // translation column first, as in the skin kernel
+        const f32x4 f = F[c * 4 + k];
+        f32x4 T = {};
+        T = __builtin_amdgcn_mfma_f32_16x16x4f32(f[0], wf[0], T, 0, 0, 0);
+        T = __builtin_amdgcn_mfma_f32_16x16x4f32(f[1], wf[1], T, 0, 0, 0);
+        T = __builtin_amdgcn_mfma_f32_16x16x4f32(f[2], wf[2], T, 0, 0, 0);
+        T = __builtin_amdgcn_mfma_f32_16x16x4f32(f[3], wf[3], T, 0, 0, 0);
+        if (k == 3) {
+          out[c] = T;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) out[c][r] = fmaf(T[r], p[k][r], out[c][r]);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int hr = row0 + r;
+      if (hr < n_valid) {
+        float o0 = out[0][r], o1 = out[1][r], o2 = out[2][r];
+        if constexpr (kTrans) {
+          o0 += trs[wave][hr * 3 + 0];
+          o1 += trs[wave][hr * 3 + 1];
+          o2 += trs[wave][hr * 3 + 2];
+        }
+        float* o = vtile + unsigned(hr * vstride32 + voff);
+        o[0] = o0;
+        o[1] = o1;
+        o[2] = o2;
+        if (ptile) {
+          float* pv = ptile + unsigned(hr * vstride32 + voff);
+          pv[0] = p[0][r];
+          pv[1] = p[1][r];
+          pv[2] = p[2][r];
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // skin: lane = vertex, wave = run of kSkinHands hands; grid (hand runs, vertex groups).
 // ---------------------------------------------------------------------------
 constexpr int kSkinHands = 16;
@@ -756,13 +922,14 @@ __global__ __launch_bounds__(256) void rodrigues_kernel(const float* __restrict_
 
 hipError_t launch_articulate(const DeviceModel& m, int64_t n, const float* betas,
                              int64_t betas_stride, const float* pose, const float* trans,
-                             float* features, float* transforms, float* tfrags, float* joints,
+                             float* features, float* transforms, float* tfrags,
+                             float* features16, float* tfrag16, float* joints,
                              float* rest_joints, float* rot_mats, hipStream_t stream) {
   const int64_t blocks = (n + kHandTile - 1) / kHandTile;
   hipLaunchKernelGGL(articulate_kernel, dim3(unsigned(blocks)), dim3(512), 0, stream, betas,
                      betas_stride, pose, trans, m.joint_template, m.joint_shape, m.parents,
-                     m.depth, m.max_depth, n, features, transforms, tfrags, joints, rest_joints,
-                     rot_mats);
+                     m.depth, m.max_depth, n, features, transforms, tfrags, features16, tfrag16,
+                     joints, rest_joints, rot_mats);
   return hipGetLastError();
 }
 
@@ -776,13 +943,13 @@ hipError_t launch_blend(const DeviceModel& m, int64_t n, const float* features, 
 }
 
 #ifndef MANO_FUSED_IMPL
-#define MANO_FUSED_IMPL 1  // 0: 8-wave LDS-staged form, 1: register-resident form
+#define MANO_FUSED_IMPL 2  // 0: 8-wave LDS-staged, 1: register-resident 32x32, 2: 16x16x4 form
 #endif
 
 hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features,
-                             const float* tfrags, const float* trans, float* verts,
-                             float* vposed, hipStream_t stream) {
-  const int64_t n_ht = (n + kHandTile - 1) / kHandTile;
+                             const float* tfrags, const float* features16, const float* tfrag16,
+                             const float* trans, float* verts, float* vposed, hipStream_t stream) {
+  [[maybe_unused]] const int64_t n_ht = (n + kHandTile - 1) / kHandTile;
 #if MANO_FUSED_IMPL == 0
   const int64_t blocks = (n_ht + kFusedWaves - 1) / kFusedWaves;
   const dim3 grid{unsigned(blocks)}, block{unsigned(kFusedWaves * 64)};
@@ -792,7 +959,7 @@ hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* featu
   else
     hipLaunchKernelGGL(blend_skin_kernel<false>, grid, block, 0, stream, features, m.basis_groups,
                        m.weight_frags, tfrags, trans, verts, vposed, n, m.n_verts, m.n_groups);
-#else
+#elif MANO_FUSED_IMPL == 1
   const int64_t blocks = (n_ht + 3) / 4;
   const dim3 grid{unsigned(blocks)}, block{256u};
   if (trans)
@@ -803,6 +970,15 @@ hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* featu
     hipLaunchKernelGGL(blend_skin_reg_kernel<false>, grid, block, 0, stream, features,
                        m.basis_groups, m.weight_frags, tfrags, trans, verts, vposed, n, m.n_verts,
                        m.n_groups);
+#else
+  const int64_t nt16 = (n + 15) / 16;
+  const dim3 grid{unsigned((nt16 + 3) / 4)}, block{256u};
+  if (trans)
+    hipLaunchKernelGGL(blend_skin16_kernel<true>, grid, block, 0, stream, features16, m.basis16,
+                       m.wfrag16, tfrag16, trans, verts, vposed, n, m.n_verts, m.n_groups16);
+  else
+    hipLaunchKernelGGL(blend_skin16_kernel<false>, grid, block, 0, stream, features16, m.basis16,
+                       m.wfrag16, tfrag16, trans, verts, vposed, n, m.n_verts, m.n_groups16);
 #endif
   return hipGetLastError();
 }

@@ -13,13 +13,18 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = {"blend_skin_kernel": "blend_skin", "blend_kernel": "blend", "skin_kernel": "skin",
-           "articulate_kernel": "articulate"}
+KERNELS = {"blend_skin_reg_kernel": "blend_skin", "blend_skin_kernel": "blend_skin",
+           "blend_kernel": "blend", "skin_kernel": "skin", "articulate_kernel": "articulate"}
+# FETCH_SIZE correction per kernel: x2 where the reads are 16-B-per-lane streams
+# (MI355X_MICROARCH.md §HBM); x1 where the dominant reads are 12-B (dwordx3) or
+# scattered, for which the raw counter already matches the algorithmic bytes
+# (skin: raw FETCH_SIZE 705 MB vs 662 MB algorithmic at 65,536 hands).
+FETCH_FACTOR = {"blend_skin": 2.0, "blend": 2.0, "skin": 1.0, "articulate": 1.0}
 
 
 def short(name):
-    for k, v in KERNELS.items():
-        if k + "<" in name or k + "(" in name:
+    for k, v in KERNELS.items():  # longest names first (dict order above)
+        if "::" + k + "<" in name or "::" + k + "(" in name:
             return v
     return None
 
@@ -40,12 +45,13 @@ def main(d):
         for c, v in sorted(avg.items()):
             print(f"    {c:32s} {v:.6g}")
         if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
-            rd = 2 * avg["FETCH_SIZE"] * 1024
+            rd = FETCH_FACTOR[k] * avg["FETCH_SIZE"] * 1024
             wr = avg["WRITE_SIZE"] * 1024
-            print(f"    -> hbm read {rd/1e6:.1f} MB (2x FETCH_SIZE), write {wr/1e6:.1f} MB per launch")
+            print(f"    -> hbm read {rd/1e6:.1f} MB ({FETCH_FACTOR[k]:g}x FETCH_SIZE), write {wr/1e6:.1f} MB per launch")
             out["kernels"][k] = {"hbm_bytes_per_launch": rd + wr, "hbm_read_bytes": rd,
                                  "hbm_write_bytes": wr, "fetch_size_kb": avg["FETCH_SIZE"],
-                                 "write_size_kb": avg["WRITE_SIZE"], "path": path}
+                                 "write_size_kb": avg["WRITE_SIZE"], "path": path,
+                                 "fetch_factor": FETCH_FACTOR[k]}
     print(json.dumps(out))
 
 
