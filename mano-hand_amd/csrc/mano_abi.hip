@@ -163,46 +163,6 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
           }
           tiles[((size_t(t) * kKGroups + g) * 64 + l) * 4 + q] = v;
         }
-  // Fused blend+skin layout: group g = 32 vertices starting at min(32g, V-32);
-  // its three tiles hold the x, y, z columns of those vertices.
-  const int n_groups = (V + 31) / 32;
-  std::vector<float> gtiles(size_t(n_groups) * 3 * kTileFloats, 0.f);
-  std::vector<float> gtmpl(size_t(n_groups) * 3 * kColTile, 0.f);
-  for (int g = 0; g < n_groups; ++g) {
-    const int vb = std::max(0, std::min(32 * g, V - 32));
-    for (int q = 0; q < 3; ++q) {
-      const size_t t = size_t(g) * 3 + q;
-      for (int c = 0; c < kColTile; ++c) {
-        const int v = vb + c;
-        if (v < V) gtmpl[t * kColTile + c] = float(mesh_template[size_t(v) * 3 + q]);
-      }
-      for (int gg = 0; gg < kKGroups; ++gg)
-        for (int l = 0; l < 64; ++l)
-          for (int qq = 0; qq < 4; ++qq) {
-            const int k = 2 * (4 * gg + qq) + (l >> 5);
-            const int v = vb + (l & 31);
-            float val = 0.f;
-            if (k <= kK && v < V) {
-              const size_t colv = size_t(v) * 3 + q;
-              val = k < kShape ? float(mesh_shape_basis[colv * kShape + k])
-                    : k < kK   ? float(mesh_pose_basis[colv * kPoseFeats + (k - kShape)])
-                               : float(mesh_template[colv]);  // row 145: template
-            }
-            gtiles[((t * kKGroups + gg) * 64 + l) * 4 + qq] = val;
-          }
-    }
-  }
-  std::vector<float> wfr(size_t(n_groups) * kWFragFloats, 0.f);
-  for (int g = 0; g < n_groups; ++g) {
-    const int vb = std::max(0, std::min(32 * g, V - 32));
-    for (int l = 0; l < 64; ++l)
-      for (int st = 0; st < 8; ++st) {
-        const int v = vb + (l & 31), jj = 2 * st + (l >> 5);
-        if (v < V)
-          wfr[size_t(g) * kWFragFloats + ((st >> 2) * 64 + l) * 4 + (st & 3)] =
-              float(skinning_weights[size_t(v) * kJoints + jj]);
-      }
-  }
   // 16x16x4 fused layout: group g = 16 vertices from min(16g, V-16).
   const int n_groups16 = (V + 15) / 16;
   std::vector<float> b16(size_t(n_groups16) * 3 * kTile16Floats, 0.f);
@@ -230,8 +190,6 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
           }
     }
   }
-  std::vector<float> tmpl(size_t(n_col_tiles) * kColTile, 0.f);
-  for (int i = 0; i < n_cols; ++i) tmpl[i] = float(mesh_template[i]);
   std::vector<float> wts(size_t(V) * kJoints);
   for (size_t i = 0; i < wts.size(); ++i) wts[i] = float(skinning_weights[i]);
   std::vector<float> pca(kPca * kPca, 0.f), pmean(kPca, 0.f), zeros(64, 0.f);
@@ -242,15 +200,19 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
 
   // ---- one device block, 256-B aligned sub-arrays ----
   struct Part { const void* src; size_t bytes; size_t off; };
-  std::vector<Part> parts = {
-      {tiles.data(), tiles.size() * 4, 0}, {tmpl.data(), tmpl.size() * 4, 0},
-      {wts.data(), wts.size() * 4, 0},     {jt.data(), jt.size() * 4, 0},
-      {js.data(), js.size() * 4, 0},       {parents, kJoints * 4, 0},
-      {depth.data(), kJoints * 4, 0},      {pca.data(), pca.size() * 4, 0},
-      {pmean.data(), pmean.size() * 4, 0}, {zeros.data(), zeros.size() * 4, 0},
-      {gtiles.data(), gtiles.size() * 4, 0}, {gtmpl.data(), gtmpl.size() * 4, 0},
-      {wfr.data(), wfr.size() * 4, 0}, {b16.data(), b16.size() * 4, 0},
-      {w16.data(), w16.size() * 4, 0}};
+  enum { kBasis, kWeights, kJt, kJs, kParents, kDepth, kPcaB, kPcaM, kZeros, kBasis16, kW16, kNParts };
+  std::vector<Part> parts(kNParts);
+  parts[kBasis] = {tiles.data(), tiles.size() * 4, 0};
+  parts[kWeights] = {wts.data(), wts.size() * 4, 0};
+  parts[kJt] = {jt.data(), jt.size() * 4, 0};
+  parts[kJs] = {js.data(), js.size() * 4, 0};
+  parts[kParents] = {parents, kJoints * 4, 0};
+  parts[kDepth] = {depth.data(), kJoints * 4, 0};
+  parts[kPcaB] = {pca.data(), pca.size() * 4, 0};
+  parts[kPcaM] = {pmean.data(), pmean.size() * 4, 0};
+  parts[kZeros] = {zeros.data(), zeros.size() * 4, 0};
+  parts[kBasis16] = {b16.data(), b16.size() * 4, 0};
+  parts[kW16] = {w16.data(), w16.size() * 4, 0};
   size_t total = 0;
   for (auto& p : parts) {
     p.off = total;
@@ -275,22 +237,18 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   m->magic = kMagic;
   m->device = device;
   m->block = block;
-  m->dm.basis_tiles = reinterpret_cast<float*>(b + parts[0].off);
-  m->dm.template_cols = reinterpret_cast<float*>(b + parts[1].off);
-  m->dm.weights = reinterpret_cast<float*>(b + parts[2].off);
-  m->dm.joint_template = reinterpret_cast<float*>(b + parts[3].off);
-  m->dm.joint_shape = reinterpret_cast<float*>(b + parts[4].off);
-  m->dm.parents = reinterpret_cast<int32_t*>(b + parts[5].off);
-  m->dm.depth = reinterpret_cast<int32_t*>(b + parts[6].off);
-  m->dm.pca_basis = reinterpret_cast<float*>(b + parts[7].off);
-  m->dm.pca_mean = reinterpret_cast<float*>(b + parts[8].off);
-  m->dm.zeros = reinterpret_cast<float*>(b + parts[9].off);
-  m->dm.basis_groups = reinterpret_cast<float*>(b + parts[10].off);
-  m->dm.template_groups = reinterpret_cast<float*>(b + parts[11].off);
-  m->dm.weight_frags = reinterpret_cast<float*>(b + parts[12].off);
-  m->dm.n_groups = n_groups;
-  m->dm.basis16 = reinterpret_cast<float*>(b + parts[13].off);
-  m->dm.wfrag16 = reinterpret_cast<float*>(b + parts[14].off);
+  auto at = [&](int i) { return reinterpret_cast<float*>(b + parts[i].off); };
+  m->dm.basis_tiles = at(kBasis);
+  m->dm.weights = at(kWeights);
+  m->dm.joint_template = at(kJt);
+  m->dm.joint_shape = at(kJs);
+  m->dm.parents = reinterpret_cast<int32_t*>(at(kParents));
+  m->dm.depth = reinterpret_cast<int32_t*>(at(kDepth));
+  m->dm.pca_basis = at(kPcaB);
+  m->dm.pca_mean = at(kPcaM);
+  m->dm.zeros = at(kZeros);
+  m->dm.basis16 = at(kBasis16);
+  m->dm.wfrag16 = at(kW16);
   m->dm.n_groups16 = n_groups16;
   m->dm.max_depth = max_depth;
   m->dm.n_verts = V;
@@ -358,7 +316,6 @@ int mano_stage_articulate(const mano_model* m, int64_t n, const float* betas,
   hipError_t e = mano::launch_articulate(
       m->dm, n, betas, betas_stride, pose, trans, reinterpret_cast<float*>(base + w.features_off),
       reinterpret_cast<float*>(base + w.transforms_off),
-      reinterpret_cast<float*>(base + w.tfrag_off),
       reinterpret_cast<float*>(base + w.features16_off),
       reinterpret_cast<float*>(base + w.tfrag16_off), joints, rest_joints, rot_mats,
       static_cast<hipStream_t>(stream));
@@ -414,9 +371,7 @@ int mano_stage_blend_skin(const mano_model* m, int64_t n, float* rest_verts, con
   const mano::Workspace w = mano::workspace_layout(m->dm, n);
   char* base = static_cast<char*>(ws);
   hipError_t e = mano::launch_blend_skin(
-      m->dm, n, reinterpret_cast<const float*>(base + w.features_off),
-      reinterpret_cast<const float*>(base + w.tfrag_off),
-      reinterpret_cast<const float*>(base + w.features16_off),
+      m->dm, n, reinterpret_cast<const float*>(base + w.features16_off),
       reinterpret_cast<const float*>(base + w.tfrag16_off), trans, verts, rest_verts,
       static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "blend_skin launch");

@@ -23,13 +23,9 @@ constexpr int kTileFloats = kKGroups * 64 * 4; // 4864 floats = 19,456 B per til
 constexpr int kHandTile = 32;                  // hands per MFMA row tile
 constexpr int kColTile = 32;                   // basis columns per MFMA col tile
 constexpr int kTransformFloats = kJoints * 12; // 3x4 skinning transform per joint
-// Fused-kernel LBS operands.  T_{c,k}[hand][v] = sum_j A_j(hand)[c][k] W[v][j]
-// is one 32x32 MFMA tile per (c, k) over K = 16 joints (8 steps of 32x32x2):
-//   A fragments, per hand tile: [c*4+k][s/4][lane][s%4] = A_{2s+(lane>>5)}(32 ht + (lane&31))[c][k]
-//   W fragments, per vertex group: [s/4][lane][s%4]     = W[vb + (lane&31)][2s + (lane>>5)]
-constexpr int kTFragFloats = 12 * 8 * 64;      // 6144 floats = 24 KB per hand tile
-constexpr int kWFragFloats = 8 * 64;           // 512 floats per vertex group
-// 16x16x4 form of the fused kernel (16-hand tiles, 16-vertex groups):
+// Fused blend_skin kernel operands (v_mfma_f32_16x16x4_f32, 16-hand tiles,
+// 16-vertex groups; the LBS transforms T_{c,k}[hand][v] = sum_j A_j[c][k] W[v][j]
+// are one 16x16 tile per (c, k) over K = 16 joints):
 //   features16 per 16 hands: [10][64][4], lane l, step s = 4g + q:
 //       X[16 t + (l & 15)][k = 4 s + (l >> 4)]            (K padded to 160)
 //   basis16 per vertex group (3 tiles x, y, z): [10][64][4]:
@@ -45,7 +41,6 @@ constexpr int kWFrag16Floats = 64 * 4;         // 256 floats per 16-vertex group
 // Device-resident model buffer (float32, layouts chosen for the kernels).
 struct DeviceModel {
   float* basis_tiles;   // [n_col_tiles][kKGroups][64][4] MFMA B fragments
-  float* template_cols; // [n_col_tiles * 32] mesh_template flattened, zero-padded
   float* weights;       // [V][16] skinning weights
   float* joint_template;// [16][3]   J_regressor . mesh_template       (float64 fold)
   float* joint_shape;   // [16][3][10] J_regressor . mesh_shape_basis (float64 fold)
@@ -54,22 +49,18 @@ struct DeviceModel {
   float* pca_basis;     // [45][45]
   float* pca_mean;      // [45]
   float* zeros;         // [64] zero vector (stand-in operand for an absent trans)
-  float* basis_groups;  // [n_groups][3][kKGroups][64][4] B tiles: x|y|z of 32 verts
-  float* template_groups; // [n_groups][3][32] template coordinate per group column
-  float* weight_frags;  // [n_groups][kWFragFloats] MFMA B fragments of W^T per group
   float* basis16;       // [n_groups16][3][kTile16Floats]
   float* wfrag16;       // [n_groups16][kWFrag16Floats]
   int32_t max_depth;
   int32_t n_verts;
   int32_t n_cols;       // 3V
   int32_t n_col_tiles;  // ceil(3V / 32)
-  int32_t n_groups;     // ceil(V / 32) vertex groups of the fused kernel (last one shifted)
   int32_t n_groups16;   // ceil(V / 16) groups of the 16x16 fused kernel (last one shifted)
 };
 
 // Workspace carving (all offsets 256-B aligned).
 struct Workspace {
-  size_t features_off, transforms_off, tfrag_off, features16_off, tfrag16_off, vposed_off, total;
+  size_t features_off, transforms_off, features16_off, tfrag16_off, vposed_off, total;
 };
 
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -79,8 +70,7 @@ inline Workspace workspace_layout(const DeviceModel& m, int64_t n) {
   const int64_t n_tiles = (n + kHandTile - 1) / kHandTile;
   w.features_off = 0;
   w.transforms_off = align256(w.features_off + size_t(n_tiles) * kTileFloats * sizeof(float));
-  w.tfrag_off = align256(w.transforms_off + size_t(n) * kTransformFloats * sizeof(float));
-  w.features16_off = align256(w.tfrag_off + size_t(n_tiles) * kTFragFloats * sizeof(float));
+  w.features16_off = align256(w.transforms_off + size_t(n) * kTransformFloats * sizeof(float));
   w.tfrag16_off = align256(w.features16_off + size_t(2 * n_tiles) * kTile16Floats * sizeof(float));
   w.vposed_off = align256(w.tfrag16_off + size_t(2 * n_tiles) * kTFrag16Floats * sizeof(float));
   w.total = align256(w.vposed_off + size_t(n) * m.n_cols * sizeof(float));
@@ -90,14 +80,14 @@ inline Workspace workspace_layout(const DeviceModel& m, int64_t n) {
 // Kernel launchers (mano_kernels.hip).  All asynchronous on `stream`.
 hipError_t launch_articulate(const DeviceModel& m, int64_t n, const float* betas,
                              int64_t betas_stride, const float* pose, const float* trans,
-                             float* features, float* transforms, float* tfrags,
-                             float* features16, float* tfrag16, float* joints,
+                             float* features, float* transforms, float* features16,
+                             float* tfrag16, float* joints,
                              float* rest_joints, float* rot_mats, hipStream_t stream);
 hipError_t launch_blend(const DeviceModel& m, int64_t n, const float* features,
                         float* vposed, hipStream_t stream);
-hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features,
-                             const float* tfrags, const float* features16, const float* tfrag16,
-                             const float* trans, float* verts, float* vposed, hipStream_t stream);
+hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features16,
+                             const float* tfrag16, const float* trans, float* verts,
+                             float* vposed, hipStream_t stream);
 hipError_t launch_skin(const DeviceModel& m, int64_t n, const float* transforms,
                        const float* vposed, const float* trans, float* verts,
                        hipStream_t stream);

@@ -67,15 +67,13 @@ __global__ __launch_bounds__(512) void articulate_kernel(
     const float* __restrict__ trans, const float* __restrict__ joint_template,
     const float* __restrict__ joint_shape, const int32_t* __restrict__ parents,
     const int32_t* __restrict__ depth, int max_depth, int64_t n,
-    float* __restrict__ features, float* __restrict__ transforms, float* __restrict__ tfrags,
+    float* __restrict__ features, float* __restrict__ transforms,
     float* __restrict__ features16, float* __restrict__ tfrag16, float* __restrict__ joints,
     float* __restrict__ rest_joints, float* __restrict__ rot_mats) {
   __shared__ f32x4 tile[kKGroups * 64];
-  __shared__ f32x4 ttile[kTFragFloats / 4];
   __shared__ f32x4 tile16[2 * kTile16Floats / 4];
   __shared__ f32x4 ttile16[2 * kTFrag16Floats / 4];
   float* tilef = reinterpret_cast<float*>(tile);
-  float* ttilef = reinterpret_cast<float*>(ttile);
   float* tile16f = reinterpret_cast<float*>(tile16);
   float* ttile16f = reinterpret_cast<float*>(ttile16);
 
@@ -156,13 +154,9 @@ __global__ __launch_bounds__(512) void articulate_kernel(
     Aj[r * 4 + 2] = Rw[r * 3 + 2];
     Aj[r * 4 + 3] = t[r] - (Rw[r * 3 + 0] * J[0] + Rw[r * 3 + 1] * J[1] + Rw[r * 3 + 2] * J[2]);
   }
-  // ... and in the fused kernel's MFMA A-fragment layout (mano_internal.h).
+  // ... and in the fused kernel's MFMA A-fragment layout (mano_internal.h):
+  // hand (hl & 15) of 16-hand tile (hl >> 4), joint j = 4 s + (lane >> 4).
   {
-    const int s = j >> 1;
-    const int ln = hl + 32 * (j & 1);
-#pragma unroll
-    for (int ck = 0; ck < 12; ++ck) ttilef[((ck * 2 + (s >> 2)) * 64 + ln) * 4 + (s & 3)] = Aj[ck];
-    // 16x16x4 layout: hand (hl & 15) of 16-hand tile (hl >> 4), joint j = 4 s16 + (l >> 4)
     const int ln16 = (hl & 15) + 16 * (j & 3);
     float* t16 = ttile16f + (hl >> 4) * kTFrag16Floats;
 #pragma unroll
@@ -217,8 +211,6 @@ __global__ __launch_bounds__(512) void articulate_kernel(
   __syncthreads();
   f32x4* dst = reinterpret_cast<f32x4*>(features + int64_t(blockIdx.x) * kTileFloats);
   for (int i = tid; i < kKGroups * 64; i += 512) dst[i] = tile[i];
-  f32x4* tdst = reinterpret_cast<f32x4*>(tfrags + int64_t(blockIdx.x) * kTFragFloats);
-  for (int i = tid; i < kTFragFloats / 4; i += 512) tdst[i] = ttile[i];
   f32x4* d16 = reinterpret_cast<f32x4*>(features16 + int64_t(blockIdx.x) * 2 * kTile16Floats);
   for (int i = tid; i < 2 * kTile16Floats / 4; i += 512) d16[i] = tile16[i];
   f32x4* t16d = reinterpret_cast<f32x4*>(tfrag16 + int64_t(blockIdx.x) * 2 * kTFrag16Floats);
@@ -323,353 +315,6 @@ __global__ __launch_bounds__(256, 2) void blend_kernel(
     __syncthreads();
   }
   if (active) store_vposed_tile(vposed, prev, h0, (n_col_tiles - 1) * kColTile + col_in_tile, n, n_cols, hi);
-}
-
-// ---------------------------------------------------------------------------
-// blend_skin: the blend GEMM with LBS fused behind it.
-//
-// On gfx950 the f32 MFMA runs on the same datapath as f32 VALU (measured: an
-// f32-MFMA wave and a VALU wave on one SIMD take the SUM of their times, bf16
-// MFMA overlaps), so the fused kernel minimises total ALU work and keeps every
-// product on MFMA, where it runs at full rate:
-//   * the blend GEMM of a 32-hand tile x 32-vertex group: three 32x32 tiles
-//     (x, y, z columns of the same 32 vertices), 73 K-steps each;
-//   * the LBS transforms T_{c,k}[hand][v] = sum_j A_j[c][k] W[v][j]: twelve
-//     32x32 tiles, 8 K-steps (16 joints) each -- 192 MACs per vertex on MFMA
-//     instead of 192 DPP-broadcast VALU FMAs at ~40 % of the VALU peak.
-// Both produce D[hand][v] with the SAME lane layout (lane = vertex, register =
-// hand), so applying T to v_posed is register-local VALU work.  Output rows
-// are staged in LDS and leave as contiguous 12-B (x, y, z) vertex stores: a
-// store of one coordinate at a 12-B stride would be written through as three
-// partial-line writes (measured 3x WRITE_SIZE).  v_posed never touches HBM.
-// T and the apply run in the same operation order as the skin kernel, so the
-// fused and unfused paths agree bit for bit.
-//
-// Block = 8 waves (2 per SIMD) x 32 hands; the 8 waves share each basis tile
-// (LDS-DMA ring of two), one barrier per tile.
-// ---------------------------------------------------------------------------
-constexpr int kGroupVerts = 32;
-constexpr int kFusedWaves = 8;
-constexpr int kStageFloats = kHandTile * kGroupVerts * 3;  // 3,072 floats = 12 KB per wave
-
-template <bool kTrans>
-__global__ __launch_bounds__(kFusedWaves * 64, 1) void blend_skin_kernel(
-    const float* __restrict__ features, const float* __restrict__ basis_groups,
-    const float* __restrict__ weight_frags, const float* __restrict__ tfrags,
-    const float* __restrict__ trans, float* __restrict__ verts, float* __restrict__ vposed,
-    int64_t n, int n_verts, int n_groups) {
-  __shared__ f32x4 bs[2][kKGroups * 64];                 // basis tile ring   38,912 B
-  __shared__ float stage[kFusedWaves][kStageFloats];     // output staging    98,304 B
-  __shared__ float trs[kFusedWaves][kHandTile * 3];      // translations       3,072 B
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t ht = int64_t(blockIdx.x) * kFusedWaves + wave;
-  const int64_t n_ht = (n + kHandTile - 1) / kHandTile;
-  const bool active = ht < n_ht;
-  const int64_t htc = active ? ht : n_ht - 1;
-  const int hi = lane >> 5;
-  const int col = lane & 31;
-  const int64_t h0 = htc * kHandTile;
-
-  float a[kKGroups * 4];
-  {
-    const f32x4* src = reinterpret_cast<const f32x4*>(features + htc * kTileFloats) + lane;
-#pragma unroll
-    for (int g = 0; g < kKGroups; ++g) {
-      const f32x4 v = src[g * 64];
-      a[4 * g + 0] = v[0];
-      a[4 * g + 1] = v[1];
-      a[4 * g + 2] = v[2];
-      a[4 * g + 3] = v[3];
-    }
-  }
-  if constexpr (kTrans) {  // the wave's 32 translations, read back at the stores
-    if (lane < kHandTile) {
-      const int64_t h = h0 + lane;
-      const int64_t hc = h < n ? h : n - 1;
-      trs[wave][lane * 3 + 0] = trans[hc * 3 + 0];
-      trs[wave][lane * 3 + 1] = trans[hc * 3 + 1];
-      trs[wave][lane * 3 + 2] = trans[hc * 3 + 2];
-    }
-  }
-  const f32x4* tf = reinterpret_cast<const f32x4*>(tfrags + htc * kTFragFloats) + lane;
-  const int vstride32 = 3 * n_verts;
-  const int64_t n_left = n - h0;
-  const int n_valid = active ? (n_left < kHandTile ? int(n_left) : kHandTile) : 0;
-  float* vtile = verts + h0 * int64_t(vstride32);
-  float* ptile = vposed ? vposed + h0 * int64_t(vstride32) : nullptr;
-  float* st = stage[wave];
-  const int n_tiles = 3 * n_groups;
-
-  stage_basis_tile<kFusedWaves>(basis_groups, 0, bs[0], wave, lane);
-  __syncthreads();
-
-  for (int grp = 0; grp < n_groups; ++grp) {
-    // The transform fragments are the same for every group; re-read them from
-    // L2 per group rather than pin 96 VGPRs (the empty asm hides the loop
-    // invariance from LICM).
-    int tfo = 0;
-    asm volatile("" : "+s"(tfo));
-    const f32x4* tfg = tf + tfo;
-    // W^T fragments of this vertex group (B operand of the LBS tiles).
-    float wf[8];
-    {
-      const f32x4* wp = reinterpret_cast<const f32x4*>(weight_frags + int64_t(grp) * kWFragFloats) + lane;
-      const f32x4 w0 = wp[0], w1 = wp[64];
-      wf[0] = w0[0]; wf[1] = w0[1]; wf[2] = w0[2]; wf[3] = w0[3];
-      wf[4] = w1[0]; wf[5] = w1[1]; wf[6] = w1[2]; wf[7] = w1[3];
-    }
-    // ---- blend GEMM: v_posed x, y, z of 32 vertices for the 32 hands ----
-    // LBS tile i = (c = i / 4, k = 3 - i % 4) uses fragments F[i & 1][0..1]
-    // (K steps 0-3 and 4-7); tile i+1's are requested while tile i runs, and
-    // tile 0's before the last GEMM tile.
-    f32x4 F[2][2];
-    f32x16 p[3];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const int t = 3 * grp + q;
-      if (t + 1 < n_tiles) stage_basis_tile<kFusedWaves>(basis_groups, t + 1, bs[(t + 1) & 1], wave, lane);
-      if (q == 2) {
-        F[0][0] = tfg[(3 * 2 + 0) * 64];
-        F[0][1] = tfg[(3 * 2 + 1) * 64];
-      }
-      p[q] = mfma_tile(a, bs[t & 1], lane);
-      __syncthreads();
-    }
-    int vb = grp * kGroupVerts;
-    if (vb > n_verts - kGroupVerts) vb = n_verts - kGroupVerts;
-    // Store-loop addressing is recomputed per group from a laundered lane id:
-    // hoisted out of the loop, its 32 loop-invariant offsets would spill.
-    int lane_g = lane;
-    asm volatile("" : "+v"(lane_g));
-    if (ptile) {  // rest_verts requested: stage and store v_posed like verts below
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int hr = (r & 3) + 8 * (r >> 2) + 4 * hi;
-          st[hr * (kGroupVerts * 3) + 3 * col + c] = p[c][r];
-        }
-      }
-#pragma unroll
-      for (int m = 0; m < 16; ++m) {
-        const int idx = m * 64 + lane_g;
-        const int hand = idx >> 5, vv = idx & 31;
-        if (hand < n_valid) {
-          const float* sp = st + hand * (kGroupVerts * 3) + 3 * vv;
-          float* o = ptile + unsigned(hand * vstride32 + 3 * (vb + vv));
-          o[0] = sp[0];
-          o[1] = sp[1];
-          o[2] = sp[2];
-        }
-      }
-    }
-    // ---- LBS: out_c = fma(T_c0, x, fma(T_c1, y, fma(T_c2, z, T_c3))) ----
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      f32x16 out;
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const int i = c * 4 + kk;
-        const int k = 3 - kk;  // translation column first, as in the skin kernel
-        if (i + 1 < 12) {
-          const int cn = (i + 1) / 4, kn = 3 - (i + 1) % 4;
-          F[(i + 1) & 1][0] = tfg[((cn * 4 + kn) * 2 + 0) * 64];
-          F[(i + 1) & 1][1] = tfg[((cn * 4 + kn) * 2 + 1) * 64];
-        }
-        const f32x4 f0 = F[i & 1][0];
-        const f32x4 f1 = F[i & 1][1];
-        f32x16 T = {};
-        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f0[0], wf[0], T, 0, 0, 0);
-        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f0[1], wf[1], T, 0, 0, 0);
-        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f0[2], wf[2], T, 0, 0, 0);
-        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f0[3], wf[3], T, 0, 0, 0);
-        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f1[0], wf[4], T, 0, 0, 0);
-        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f1[1], wf[5], T, 0, 0, 0);
-        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f1[2], wf[6], T, 0, 0, 0);
-        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f1[3], wf[7], T, 0, 0, 0);
-        if (k == 3) {
-          out = T;
-        } else {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) out[r] = fmaf(T[r], p[k][r], out[r]);
-        }
-      }
-      // stage component c: row = hand (register r), 3 floats per vertex (lane)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int hr = (r & 3) + 8 * (r >> 2) + 4 * hi;
-        float o = out[r];
-        if constexpr (kTrans) o += trs[wave][hr * 3 + c];
-        st[hr * (kGroupVerts * 3) + 3 * col + c] = o;
-      }
-    }
-    // ---- contiguous stores: 16 (hand, vertex) points per lane, 12 B each ----
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      if ((m & 3) == 0) __builtin_amdgcn_sched_barrier(0);
-      const int idx = m * 64 + lane_g;
-      const int hand = idx >> 5, vv = idx & 31;
-      if (hand < n_valid) {
-        const float* sp = st + hand * (kGroupVerts * 3) + 3 * vv;
-        float* o = vtile + unsigned(hand * vstride32 + 3 * (vb + vv));
-        o[0] = sp[0];
-        o[1] = sp[1];
-        o[2] = sp[2];
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// blend_skin, register-resident form: 4 waves per block, one wave per SIMD and
-// the whole 512-entry register file per wave -- the 32 hands' transform
-// fragments stay in VGPRs for all vertex groups, the three output components
-// of a vertex are in registers together, so each lane stores contiguous 12-B
-// (x, y, z) points straight to HBM with no LDS staging.
-// ---------------------------------------------------------------------------
-template <bool kTrans>
-__global__ __launch_bounds__(256, 1) void blend_skin_reg_kernel(
-    const float* __restrict__ features, const float* __restrict__ basis_groups,
-    const float* __restrict__ weight_frags, const float* __restrict__ tfrags,
-    const float* __restrict__ trans, float* __restrict__ verts, float* __restrict__ vposed,
-    int64_t n, int n_verts, int n_groups) {
-  __shared__ f32x4 bs[2][kKGroups * 64];
-  __shared__ float trs[4][kHandTile * 3];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t ht = int64_t(blockIdx.x) * 4 + wave;
-  const int64_t n_ht = (n + kHandTile - 1) / kHandTile;
-  const bool active = ht < n_ht;
-  const int64_t htc = active ? ht : n_ht - 1;
-  const int hi = lane >> 5;
-  const int col = lane & 31;
-  const int64_t h0 = htc * kHandTile;
-
-  float a[kKGroups * 4];
-  {
-    const f32x4* src = reinterpret_cast<const f32x4*>(features + htc * kTileFloats) + lane;
-#pragma unroll
-    for (int g = 0; g < kKGroups; ++g) {
-      const f32x4 v = src[g * 64];
-      a[4 * g + 0] = v[0];
-      a[4 * g + 1] = v[1];
-      a[4 * g + 2] = v[2];
-      a[4 * g + 3] = v[3];
-    }
-  }
-  if constexpr (kTrans) {
-    if (lane < kHandTile) {
-      const int64_t h = h0 + lane;
-      const int64_t hc = h < n ? h : n - 1;
-      trs[wave][lane * 3 + 0] = trans[hc * 3 + 0];
-      trs[wave][lane * 3 + 1] = trans[hc * 3 + 1];
-      trs[wave][lane * 3 + 2] = trans[hc * 3 + 2];
-    }
-  }
-  const f32x4* tf = reinterpret_cast<const f32x4*>(tfrags + htc * kTFragFloats) + lane;
-  const int vstride32 = 3 * n_verts;
-  const int64_t n_left = n - h0;
-  const int n_valid = active ? (n_left < kHandTile ? int(n_left) : kHandTile) : 0;
-  float* vtile = verts + h0 * int64_t(vstride32);
-  float* ptile = vposed ? vposed + h0 * int64_t(vstride32) : nullptr;
-  const int n_tiles = 3 * n_groups;
-
-  stage_basis_tile(basis_groups, 0, bs[0], wave, lane);
-  __syncthreads();
-
-  for (int grp = 0; grp < n_groups; ++grp) {
-    // Transform fragments (the same for every group) stream from L2 one LBS
-    // tile ahead; the empty asm keeps LICM from pinning all 96 VGPRs of them.
-    int tfo = 0;
-    asm volatile("" : "+s"(tfo));
-    const f32x4* tfg = tf + tfo;
-    float wf[8];
-    {
-      const f32x4* wp = reinterpret_cast<const f32x4*>(weight_frags + int64_t(grp) * kWFragFloats) + lane;
-      const f32x4 w0 = wp[0], w1 = wp[64];
-      wf[0] = w0[0]; wf[1] = w0[1]; wf[2] = w0[2]; wf[3] = w0[3];
-      wf[4] = w1[0]; wf[5] = w1[1]; wf[6] = w1[2]; wf[7] = w1[3];
-    }
-    f32x4 F[2][2];
-    f32x16 p[3];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const int t = 3 * grp + q;
-      if (t + 1 < n_tiles) stage_basis_tile(basis_groups, t + 1, bs[(t + 1) & 1], wave, lane);
-      if (q == 2) {  // LBS tile 0 = (c 0, k 3)
-        F[0][0] = tfg[(3 * 2 + 0) * 64];
-        F[0][1] = tfg[(3 * 2 + 1) * 64];
-      }
-      p[q] = mfma_tile(a, bs[t & 1], lane);
-      __syncthreads();
-    }
-    int vb = grp * kGroupVerts;
-    if (vb > n_verts - kGroupVerts) vb = n_verts - kGroupVerts;
-    const int voff = 3 * (vb + col);
-    if (ptile) {  // rest_verts requested: store v_posed before p starts dying
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int hr = (r & 3) + 8 * (r >> 2) + 4 * hi;
-        if (hr < n_valid) {
-          float* pv = ptile + unsigned(hr * vstride32 + voff);
-          pv[0] = p[0][r];
-          pv[1] = p[1][r];
-          pv[2] = p[2][r];
-        }
-      }
-    }
-    f32x16 out[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const int i = c * 4 + kk;
-        const int k = 3 - kk;  // translation column first, as in the skin kernel
-        if (i + 1 < 12) {
-          const int cn = (i + 1) / 4, kn = 3 - (i + 1) % 4;
-          F[(i + 1) & 1][0] = tfg[((cn * 4 + kn) * 2 + 0) * 64];
-          F[(i + 1) & 1][1] = tfg[((cn * 4 + kn) * 2 + 1) * 64];
-        }
-        const f32x4 f0 = F[i & 1][0];
-        const f32x4 f1 = F[i & 1][1];
-        f32x16 T = {};
-        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f0[0], wf[0], T, 0, 0, 0);
-        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f0[1], wf[1], T, 0, 0, 0);
-        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f0[2], wf[2], T, 0, 0, 0);
-        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f0[3], wf[3], T, 0, 0, 0);
-        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f1[0], wf[4], T, 0, 0, 0);
-        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f1[1], wf[5], T, 0, 0, 0);
-        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f1[2], wf[6], T, 0, 0, 0);
-        T = __builtin_amdgcn_mfma_f32_32x32x2f32(f1[3], wf[7], T, 0, 0, 0);
-        if (k == 3) {
-          out[c] = T;
-        } else {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) out[c][r] = fmaf(T[r], p[k][r], out[c][r]);
-        }
-        // One LBS tile in flight at a time: left alone, the scheduler issues
-        // all twelve 8-MFMA chains first and keeps 192 VGPRs of results live.
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int hr = (r & 3) + 8 * (r >> 2) + 4 * hi;
-      if (hr < n_valid) {
-        float o0 = out[0][r], o1 = out[1][r], o2 = out[2][r];
-        if constexpr (kTrans) {
-          o0 += trs[wave][hr * 3 + 0];
-          o1 += trs[wave][hr * 3 + 1];
-          o2 += trs[wave][hr * 3 + 2];
-        }
-        float* o = vtile + unsigned(hr * vstride32 + voff);
-        o[0] = o0;
-        o[1] = o1;
-        o[2] = o2;
-      }
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -922,14 +567,14 @@ __global__ __launch_bounds__(256) void rodrigues_kernel(const float* __restrict_
 
 hipError_t launch_articulate(const DeviceModel& m, int64_t n, const float* betas,
                              int64_t betas_stride, const float* pose, const float* trans,
-                             float* features, float* transforms, float* tfrags,
-                             float* features16, float* tfrag16, float* joints,
+                             float* features, float* transforms, float* features16,
+                             float* tfrag16, float* joints,
                              float* rest_joints, float* rot_mats, hipStream_t stream) {
   const int64_t blocks = (n + kHandTile - 1) / kHandTile;
   hipLaunchKernelGGL(articulate_kernel, dim3(unsigned(blocks)), dim3(512), 0, stream, betas,
                      betas_stride, pose, trans, m.joint_template, m.joint_shape, m.parents,
-                     m.depth, m.max_depth, n, features, transforms, tfrags, features16, tfrag16,
-                     joints, rest_joints, rot_mats);
+                     m.depth, m.max_depth, n, features, transforms, features16, tfrag16, joints,
+                     rest_joints, rot_mats);
   return hipGetLastError();
 }
 
@@ -942,35 +587,9 @@ hipError_t launch_blend(const DeviceModel& m, int64_t n, const float* features, 
   return hipGetLastError();
 }
 
-#ifndef MANO_FUSED_IMPL
-#define MANO_FUSED_IMPL 2  // 0: 8-wave LDS-staged, 1: register-resident 32x32, 2: 16x16x4 form
-#endif
-
-hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features,
-                             const float* tfrags, const float* features16, const float* tfrag16,
-                             const float* trans, float* verts, float* vposed, hipStream_t stream) {
-  [[maybe_unused]] const int64_t n_ht = (n + kHandTile - 1) / kHandTile;
-#if MANO_FUSED_IMPL == 0
-  const int64_t blocks = (n_ht + kFusedWaves - 1) / kFusedWaves;
-  const dim3 grid{unsigned(blocks)}, block{unsigned(kFusedWaves * 64)};
-  if (trans)
-    hipLaunchKernelGGL(blend_skin_kernel<true>, grid, block, 0, stream, features, m.basis_groups,
-                       m.weight_frags, tfrags, trans, verts, vposed, n, m.n_verts, m.n_groups);
-  else
-    hipLaunchKernelGGL(blend_skin_kernel<false>, grid, block, 0, stream, features, m.basis_groups,
-                       m.weight_frags, tfrags, trans, verts, vposed, n, m.n_verts, m.n_groups);
-#elif MANO_FUSED_IMPL == 1
-  const int64_t blocks = (n_ht + 3) / 4;
-  const dim3 grid{unsigned(blocks)}, block{256u};
-  if (trans)
-    hipLaunchKernelGGL(blend_skin_reg_kernel<true>, grid, block, 0, stream, features,
-                       m.basis_groups, m.weight_frags, tfrags, trans, verts, vposed, n, m.n_verts,
-                       m.n_groups);
-  else
-    hipLaunchKernelGGL(blend_skin_reg_kernel<false>, grid, block, 0, stream, features,
-                       m.basis_groups, m.weight_frags, tfrags, trans, verts, vposed, n, m.n_verts,
-                       m.n_groups);
-#else
+hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features16,
+                             const float* tfrag16, const float* trans, float* verts,
+                             float* vposed, hipStream_t stream) {
   const int64_t nt16 = (n + 15) / 16;
   const dim3 grid{unsigned((nt16 + 3) / 4)}, block{256u};
   if (trans)
@@ -979,7 +598,6 @@ hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* featu
   else
     hipLaunchKernelGGL(blend_skin16_kernel<false>, grid, block, 0, stream, features16, m.basis16,
                        m.wfrag16, tfrag16, trans, verts, vposed, n, m.n_verts, m.n_groups16);
-#endif
   return hipGetLastError();
 }
 

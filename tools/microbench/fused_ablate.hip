@@ -1,5 +1,5 @@
 // Ablation timing of the fused blend_skin kernel (diagnostic only).
-// Built three times: default, -DMANO_ABLATE_NO_S (M waves only), -DMANO_ABLATE_NO_M (S waves only).
+// Times launch_blend_skin alone on random operands (WITH_TRANS=1 adds a translation).
 #include "../../mano-hand_amd/csrc/mano_kernels.hip"
 #include <cstdio>
 #include <cstdlib>
@@ -14,31 +14,24 @@ static float* dev_rand(size_t n, float scale) {
 int main(int argc, char** argv) {
   const long n = argc > 1 ? atol(argv[1]) : 65536;
   DeviceModel m{};
-  m.n_verts = 778; m.n_cols = 2334; m.n_col_tiles = 73; m.n_groups = 25;
-  m.basis_groups = dev_rand(size_t(75) * kTileFloats, 0.01f);
-  m.template_groups = dev_rand(75 * 32, 0.1f);
-  m.weights = dev_rand(778 * 16, 0.1f);
-  m.zeros = dev_rand(64, 0.f);
-  const long nt = (n + 31) / 32;
-  float* feats = dev_rand(size_t(nt) * kTileFloats, 1.f);
-  float* A = dev_rand(size_t(nt) * kTFragFloats, 1.f);
-  m.weight_frags = dev_rand(size_t(25) * kWFragFloats, 0.1f);
+  m.n_verts = 778; m.n_cols = 2334; m.n_col_tiles = 73;
   m.n_groups16 = 49;
   m.basis16 = dev_rand(size_t(147) * kTile16Floats, 0.01f);
   m.wfrag16 = dev_rand(size_t(49) * kWFrag16Floats, 0.1f);
-  float* f16 = dev_rand(size_t(2 * nt) * kTile16Floats, 1.f);
-  float* t16 = dev_rand(size_t(2 * nt) * kTFrag16Floats, 1.f);
+  const long nt16 = (n + 15) / 16;
+  float* f16 = dev_rand(size_t(nt16) * kTile16Floats, 1.f);
+  float* t16 = dev_rand(size_t(nt16) * kTFrag16Floats, 1.f);
   float* tr = dev_rand(size_t(n) * 3, 1.f);
   const bool with_trans = getenv("WITH_TRANS") != nullptr;
   float* verts; CK(hipMalloc(&verts, size_t(n) * 2334 * 4));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  for (int i = 0; i < 3; ++i) CK(launch_blend_skin(m, n, feats, A, f16, t16, with_trans ? tr : nullptr, verts, nullptr, 0));
+  for (int i = 0; i < 3; ++i) CK(launch_blend_skin(m, n, f16, t16, with_trans ? tr : nullptr, verts, nullptr, 0));
   CK(hipDeviceSynchronize());
   CK(hipEventRecord(e0));
   const int it = 20;
-  for (int i = 0; i < it; ++i) CK(launch_blend_skin(m, n, feats, A, f16, t16, with_trans ? tr : nullptr, verts, nullptr, 0));
+  for (int i = 0; i < it; ++i) CK(launch_blend_skin(m, n, f16, t16, with_trans ? tr : nullptr, verts, nullptr, 0));
   CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
   float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-  printf("%-24s n=%ld  %.3f ms\n", argc > 2 ? argv[2] : "blend_skin", n, ms / it);
+  printf("%-24s n=%ld  %.3f ms\n", argc > 2 ? argv[2] : "blend_skin16", n, ms / it);
   return 0;
 }
