@@ -2,7 +2,8 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--gather]
 
-One step = one forward (articulate -> blend GEMM -> skin) over B hands per GPU
+One step = one forward pass (articulate -> blend GEMM -> LBS; by default the
+single fused launch mano_forward) over B hands per GPU
 (BASELINE.json configs[1]: 65,536 hands, fp32 full pose, random betas), inputs
 resident in HBM before the timed region.  N > 1 runs one process per GPU
 (torch.distributed.run); shards are independent (no collective on the hot
@@ -46,8 +47,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=65536, help="hands per GPU per step")
     ap.add_argument("--gather", action="store_true", help="RCCL gather of verts+joints to GPU 0")
-    ap.add_argument("--path", choices=("fused", "unfused"), default="fused",
-                    help="fused: articulate + blend_skin (default); unfused: articulate + blend + skin")
+    ap.add_argument("--path", choices=("fused", "staged", "unfused"), default="fused",
+                    help="fused: one launch (default); staged: articulate + blend_skin; "
+                         "unfused: articulate + blend + skin")
     ap.add_argument("--model", default=None, help="dump_model.py pickle (default: synthetic seed 0)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
@@ -117,29 +119,37 @@ def main():
     pose = 0.5 * torch.randn((B, 16, 3), generator=g, device=dev)
     verts = torch.empty((B, V, 3), device=dev)
     joints = torch.empty((B, 16, 3), device=dev)
-    model.workspace(B)
     stream = torch.cuda.current_stream(dev)
+    out = {"verts": verts, "joints": joints}
+    if args.path != "fused":
+        model.workspace(B)
 
-    fused = args.path == "fused"
-
-    def step(evs=None):
-        if evs is not None:
-            evs[0].record(stream)
-        model.stage_articulate(betas, pose, joints=joints)
-        if evs is not None:
-            evs[1].record(stream)
-        if fused:
+    # Launch sequence of one step; `marks` get an event after each kernel.
+    def run_path(path, marks=None):
+        def mark(i):
+            if marks is not None:
+                marks[i].record(stream)
+        mark(0)
+        if path == "fused":  # one launch: articulate + blend GEMM + LBS
+            model.forward(betas, pose, joints=True, out=out)
+            mark(1)
+        elif path == "staged":  # articulate, then blend GEMM + LBS
+            model.stage_articulate(betas, pose, joints=joints)
+            mark(1)
             model.stage_blend_skin(B, verts)
-            if evs is not None:
-                evs[2].record(stream)
-                evs[3].record(stream)
-        else:
+            mark(2)
+        else:  # articulate, blend GEMM (v_posed to HBM), LBS
+            model.stage_articulate(betas, pose, joints=joints)
+            mark(1)
             model.stage_blend(B)
-            if evs is not None:
-                evs[2].record(stream)
+            mark(2)
             model.stage_skin(B, verts)
-            if evs is not None:
-                evs[3].record(stream)
+            mark(3)
+
+    n_marks = {"fused": 2, "staged": 3, "unfused": 4}
+
+    def step(marks=None):
+        run_path(args.path, marks)
         if args.gather and world > 1:
             if args.backend == "nccl":  # RCCL over xGMI, device to device
                 gather_to_root(verts, B * world, root=0)
@@ -151,7 +161,8 @@ def main():
         step()
     torch.cuda.synchronize()
 
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(n_marks[args.path])]
+              for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -170,50 +181,78 @@ def main():
     def span(a, b, evs):
         return float(np.mean([e[a].elapsed_time(e[b]) for e in evs]))
 
-    kernels = {"articulate": {"ms": span(0, 1, events), "bound": "latency"}}
-    kernels["articulate"]["achieved_GBs"] = ARTICULATE_BYTES_PER_HAND * B / (kernels["articulate"]["ms"] * 1e-3) / 1e9
-    if fused:
-        ms_bs = span(1, 2, events)
-        # algorithmic MFMA work of the fused kernel: blend GEMM + LBS transform blend
-        ach = FUSED_MFMA_FLOP_PER_HAND * B / (ms_bs * 1e-3) / 1e12
-        kernels["blend_skin"] = {"ms": ms_bs, "bound": "mfma", "achieved_TFLOPs": ach,
-                                 "frac": ach / PEAK_FP32_TFLOPS,
-                                 "flop_per_hand": FUSED_MFMA_FLOP_PER_HAND,
-                                 "blend_gemm_TFLOPs": BLEND_FLOP_PER_HAND * B / (ms_bs * 1e-3) / 1e12}
-        roof = {"kernel": "blend_skin16_kernel", "bound": "mfma", "achieved": ach,
-                "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_FP32_TFLOPS,
-                "traffic": load_traffic(args.pmc, "blend_skin", B)}
-        # The unfused kernels, timed on the same stream after the timed region
-        # (not part of `value`): the standalone MFMA blend and the HBM-bound LBS.
-        uev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(5)]
-        for e in [None] + uev:
-            if e is not None:
-                e[0].record(stream)
-            model.stage_blend(B)
-            if e is not None:
-                e[1].record(stream)
-            model.stage_skin(B, verts)
-            if e is not None:
-                e[2].record(stream)
-        torch.cuda.synchronize()
-        ms_b, ms_s = span(0, 1, uev), span(1, 2, uev)
+    # Per-kernel table.  The timed path's kernels come from the timed steps;
+    # the other paths' kernels are timed on the same stream afterwards (not
+    # part of `value`), so every kernel's roofline is reported each run.
+    timed = {"fused": {"forward": (0, 1)},
+             "staged": {"articulate": (0, 1), "blend_skin": (1, 2)},
+             "unfused": {"articulate": (0, 1), "blend": (1, 2), "skin": (2, 3)}}
+    ms = {k: span(a, b, events) for k, (a, b) in timed[args.path].items()}
+    if rank == 0:
+        if args.path != "fused":
+            model.workspace(B)
+        for path in ("fused", "staged", "unfused"):
+            if path == args.path:
+                continue
+            evs = [[torch.cuda.Event(enable_timing=True) for _ in range(n_marks[path])]
+                   for _ in range(5)]
+            run_path(path)
+            for e in evs:
+                run_path(path, e)
+            torch.cuda.synchronize()
+            for k, (a, b) in timed[path].items():
+                ms.setdefault(k, span(a, b, evs))
+
+    def tflops(flop, t):
+        return flop * B / (t * 1e-3) / 1e12
+
+    def gbs(nbytes, t):
+        return nbytes * B / (t * 1e-3) / 1e9
+
+    kernels = {}
+    if "forward" in ms:
+        a = tflops(FUSED_MFMA_FLOP_PER_HAND, ms["forward"])
+        kernels["forward"] = {"kernel": "blend_skin16_kernel<*, true>", "ms": ms["forward"],
+                              "bound": "mfma", "achieved_TFLOPs": a, "frac": a / PEAK_FP32_TFLOPS,
+                              "flop_per_hand": FUSED_MFMA_FLOP_PER_HAND,
+                              "in_timed_path": args.path == "fused"}
+    if "articulate" in ms:
+        a = gbs(ARTICULATE_BYTES_PER_HAND, ms["articulate"])
+        kernels["articulate"] = {"kernel": "articulate_kernel", "ms": ms["articulate"],
+                                 "bound": "latency", "achieved_GBs": a,
+                                 "in_timed_path": args.path != "fused"}
+    if "blend_skin" in ms:
+        a = tflops(FUSED_MFMA_FLOP_PER_HAND, ms["blend_skin"])
+        kernels["blend_skin"] = {"kernel": "blend_skin16_kernel<*, false>", "ms": ms["blend_skin"],
+                                 "bound": "mfma", "achieved_TFLOPs": a,
+                                 "frac": a / PEAK_FP32_TFLOPS,
+                                 "in_timed_path": args.path == "staged"}
+    if "blend" in ms:
+        a = tflops(BLEND_FLOP_PER_HAND, ms["blend"])
+        kernels["blend"] = {"kernel": "blend_kernel", "ms": ms["blend"], "bound": "mfma",
+                            "achieved_TFLOPs": a, "frac": a / PEAK_FP32_TFLOPS,
+                            "in_timed_path": args.path == "unfused"}
+    if "skin" in ms:
+        a = gbs(SKIN_BYTES_PER_HAND, ms["skin"])
+        kernels["skin"] = {"kernel": "skin16_kernel", "ms": ms["skin"], "bound": "hbm",
+                           "achieved_GBs": a, "frac": a / PEAK_HBM_GBS,
+                           "in_timed_path": args.path == "unfused"}
+
+    # Roofline of the dominant kernel of the timed path.
+    dominant = {"fused": "forward", "staged": "blend_skin"}.get(args.path)
+    if dominant is None:
+        dominant = "blend" if ms["blend"] >= ms["skin"] else "skin"
+    kd = kernels[dominant]
+    if kd["bound"] == "mfma":
+        roof = {"kernel": kd["kernel"], "bound": "mfma", "achieved": kd["achieved_TFLOPs"],
+                "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": kd["frac"]}
     else:
-        ms_b, ms_s = span(1, 2, events), span(2, 3, events)
-    ach_b = BLEND_FLOP_PER_HAND * B / (ms_b * 1e-3) / 1e12
-    ach_s = SKIN_BYTES_PER_HAND * B / (ms_s * 1e-3) / 1e9
-    kernels["blend"] = {"ms": ms_b, "bound": "mfma", "achieved_TFLOPs": ach_b,
-                        "frac": ach_b / PEAK_FP32_TFLOPS, "in_timed_path": not fused}
-    kernels["skin"] = {"ms": ms_s, "bound": "hbm", "achieved_GBs": ach_s,
-                       "frac": ach_s / PEAK_HBM_GBS, "in_timed_path": not fused}
-    if not fused:
-        if ms_b >= ms_s:
-            roof = {"kernel": "blend_kernel", "bound": "mfma", "achieved": ach_b,
-                    "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": ach_b / PEAK_FP32_TFLOPS,
-                    "traffic": load_traffic(args.pmc, "blend", B)}
-        else:
-            roof = {"kernel": "skin_kernel", "bound": "hbm", "achieved": ach_s, "peak": PEAK_HBM_GBS,
-                    "unit": "GB/s", "frac": ach_s / PEAK_HBM_GBS,
-                    "traffic": load_traffic(args.pmc, "skin", B)}
+        roof = {"kernel": kd["kernel"], "bound": "hbm", "achieved": kd["achieved_GBs"],
+                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": kd["frac"]}
+    roof["traffic"] = load_traffic(args.pmc, dominant, B)
+    roof["algorithmic_per_hand"] = (FUSED_MFMA_FLOP_PER_HAND if dominant in ("forward", "blend_skin")
+                                    else BLEND_FLOP_PER_HAND if dominant == "blend"
+                                    else SKIN_BYTES_PER_HAND)
 
     if rank == 0:
         total = B * world * args.steps

@@ -75,9 +75,10 @@ int mano_model_destroy(mano_model* model);
 /* Vertex count and device of a model. */
 int mano_model_info(const mano_model* model, int32_t* n_verts, int32_t* device);
 
-/* Device workspace (bytes) for n_hands: `mano_workspace_bytes` covers every
- * call (the unfused stages keep v_posed in it), `mano_forward_workspace_bytes`
- * only what mano_forward / articulate / blend_skin use. */
+/* Device workspace (bytes) for n_hands that the mano_stage_* calls need
+ * (`mano_workspace_bytes`; the unfused stages keep v_posed in it).
+ * `mano_forward_workspace_bytes` is 0: mano_forward is a single launch that
+ * keeps every intermediate on chip (its workspace arguments are ignored). */
 size_t mano_workspace_bytes(const mano_model* model, int64_t n_hands);
 size_t mano_forward_workspace_bytes(const mano_model* model, int64_t n_hands);
 
@@ -88,17 +89,19 @@ int mano_workspace_offsets(const mano_model* model, int64_t n_hands,
                            size_t* vposed_off);
 
 /* The full forward pass: MANOModel.update() (mano_np.py:79-115) for n_hands
- * independent hands = articulate + blend_skin.  verts is required; joints,
- * rest_verts, rest_joints, rot_mats and trans are nullable.  v_posed never
- * touches HBM unless rest_verts is requested. */
+ * independent hands, one kernel launch (articulate + blend + skin fused; same
+ * results as the staged calls bit for bit).  verts is required; joints,
+ * rest_verts, rest_joints, rot_mats and trans are nullable; betas_stride 0
+ * shares one beta row.  v_posed never touches HBM unless rest_verts is
+ * requested.  workspace / workspace_bytes are unused (may be NULL / 0). */
 int mano_forward(const mano_model* model, int64_t n_hands,
                  const float* betas, int64_t betas_stride, const float* pose,
                  const float* trans, float* verts, float* joints,
                  float* rest_verts, float* rest_joints, float* rot_mats,
                  void* workspace, size_t workspace_bytes, void* stream);
 
-/* The three kernels of mano_forward, callable one at a time (same workspace
- * carving), so each can be timed and checked alone.
+/* The forward pass as separate kernels, callable one at a time (workspace of
+ * mano_workspace_bytes), so each can be timed and its intermediates checked.
  *  articulate: Rodrigues (mano_np.py:117-148) + joint regression (:83) +
  *              pose features (:87-91) + kinematic chain (:96-104) +
  *              rest-pose removal (:106-110).

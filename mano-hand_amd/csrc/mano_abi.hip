@@ -122,6 +122,9 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   if (device >= n_dev) return fail(MANO_EINVAL, "device %d >= device count %d", device, n_dev);
   DeviceGuard guard(device);
   if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
+  int n_cu = 0;
+  e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
+  if (e != hipSuccess) return hip_fail(e, "hipDeviceGetAttribute(multiprocessor count)");
 
   const int V = n_verts;
   const int n_cols = 3 * V;
@@ -254,6 +257,7 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   m->dm.n_verts = V;
   m->dm.n_cols = n_cols;
   m->dm.n_col_tiles = n_col_tiles;
+  m->dm.n_cu = n_cu;
   *out = m;
   return MANO_OK;
 }
@@ -283,8 +287,9 @@ size_t mano_workspace_bytes(const mano_model* m, int64_t n) {
 }
 
 size_t mano_forward_workspace_bytes(const mano_model* m, int64_t n) {
-  if (check_model(m) || n < 0) return 0;
-  return mano::workspace_layout(m->dm, n).vposed_off;
+  (void)m;
+  (void)n;
+  return 0;  // mano_forward is one launch that keeps every intermediate on chip
 }
 
 int mano_workspace_offsets(const mano_model* m, int64_t n, size_t* features_off,
@@ -316,8 +321,7 @@ int mano_stage_articulate(const mano_model* m, int64_t n, const float* betas,
   hipError_t e = mano::launch_articulate(
       m->dm, n, betas, betas_stride, pose, trans, reinterpret_cast<float*>(base + w.features_off),
       reinterpret_cast<float*>(base + w.transforms_off),
-      reinterpret_cast<float*>(base + w.features16_off),
-      reinterpret_cast<float*>(base + w.tfrag16_off), joints, rest_joints, rot_mats,
+      reinterpret_cast<float*>(base + w.features16_off), joints, rest_joints, rot_mats,
       static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "articulate launch");
   return MANO_OK;
@@ -372,7 +376,7 @@ int mano_stage_blend_skin(const mano_model* m, int64_t n, float* rest_verts, con
   char* base = static_cast<char*>(ws);
   hipError_t e = mano::launch_blend_skin(
       m->dm, n, reinterpret_cast<const float*>(base + w.features16_off),
-      reinterpret_cast<const float*>(base + w.tfrag16_off), trans, verts, rest_verts,
+      reinterpret_cast<const float*>(base + w.transforms_off), trans, verts, rest_verts,
       static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "blend_skin launch");
   return MANO_OK;
@@ -382,13 +386,22 @@ int mano_forward(const mano_model* m, int64_t n, const float* betas, int64_t bet
                  const float* pose, const float* trans, float* verts, float* joints,
                  float* rest_verts, float* rest_joints, float* rot_mats, void* ws,
                  size_t ws_bytes, void* stream) {
-  g_last_error.clear();
+  (void)ws;
+  (void)ws_bytes;
   if (int rc = check_model(m)) return rc;
-  if (n > 0 && !verts) return fail(MANO_EINVAL, "verts is required");
-  if (int rc = mano_stage_articulate(m, n, betas, betas_stride, pose, trans, joints, rest_joints,
-                                     rot_mats, ws, ws_bytes, stream))
-    return rc;
-  return mano_stage_blend_skin(m, n, rest_verts, trans, verts, ws, ws_bytes, stream);
+  if (n < 0 || n > kMaxHands) return fail(MANO_EINVAL, "n_hands %lld out of range", (long long)n);
+  if (n == 0) return MANO_OK;
+  if (!verts) return fail(MANO_EINVAL, "verts is required");
+  if (!betas || !pose) return fail(MANO_EINVAL, "betas and pose are required");
+  if (betas_stride != 0 && betas_stride < mano::kShape)
+    return fail(MANO_EINVAL, "betas_stride %lld must be 0 or >= 10", (long long)betas_stride);
+  DeviceGuard guard(m->device);
+  if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
+  hipError_t e = mano::launch_forward(m->dm, n, betas, betas_stride, pose, trans, verts, joints,
+                                      rest_verts, rest_joints, rot_mats,
+                                      static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "forward launch");
+  return MANO_OK;
 }
 
 int mano_pose_from_pca(const mano_model* m, int64_t n, const float* pca, int32_t n_comps,

@@ -30,12 +30,12 @@ constexpr int kTransformFloats = kJoints * 12; // 3x4 skinning transform per joi
 //       X[16 t + (l & 15)][k = 4 s + (l >> 4)]            (K padded to 160)
 //   basis16 per vertex group (3 tiles x, y, z): [10][64][4]:
 //       B[k = 4 s + (l >> 4)][3 (vb + (l & 15)) + coord]
-//   tfrag16 per 16 hands: [12 (c*4+k)][64][4]: A_{4 s + (l >> 4)}(16 t + (l & 15))[c][k]
+//   LBS A fragments per 16 hands (read from the [n][16][3][4] transforms):
+//       F_{c,k}[q] = A_{4 q + (l >> 4)}(16 t + (l & 15))[c][k]
 //   wfrag16 per vertex group: [64][4]: W[vb + (l & 15)][4 s + (l >> 4)]
 constexpr int kSteps16 = (kK + 1 + 3) / 4;     // 37 MFMA steps (K = 146 -> 148)
 constexpr int kGroups16 = (kSteps16 + 3) / 4;  // 10 float4 groups per lane
 constexpr int kTile16Floats = kGroups16 * 64 * 4;   // 2560 floats = 10 KB
-constexpr int kTFrag16Floats = 12 * 64 * 4;    // 3072 floats = 12 KB per 16 hands
 constexpr int kWFrag16Floats = 64 * 4;         // 256 floats per 16-vertex group
 
 // Device-resident model buffer (float32, layouts chosen for the kernels).
@@ -56,11 +56,12 @@ struct DeviceModel {
   int32_t n_cols;       // 3V
   int32_t n_col_tiles;  // ceil(3V / 32)
   int32_t n_groups16;   // ceil(V / 16) groups of the 16x16 fused kernel (last one shifted)
+  int32_t n_cu;         // compute units of the device (sizes the persistent grids)
 };
 
 // Workspace carving (all offsets 256-B aligned).
 struct Workspace {
-  size_t features_off, transforms_off, features16_off, tfrag16_off, vposed_off, total;
+  size_t features_off, transforms_off, features16_off, vposed_off, total;
 };
 
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -71,8 +72,7 @@ inline Workspace workspace_layout(const DeviceModel& m, int64_t n) {
   w.features_off = 0;
   w.transforms_off = align256(w.features_off + size_t(n_tiles) * kTileFloats * sizeof(float));
   w.features16_off = align256(w.transforms_off + size_t(n) * kTransformFloats * sizeof(float));
-  w.tfrag16_off = align256(w.features16_off + size_t(2 * n_tiles) * kTile16Floats * sizeof(float));
-  w.vposed_off = align256(w.tfrag16_off + size_t(2 * n_tiles) * kTFrag16Floats * sizeof(float));
+  w.vposed_off = align256(w.features16_off + size_t(2 * n_tiles) * kTile16Floats * sizeof(float));
   w.total = align256(w.vposed_off + size_t(n) * m.n_cols * sizeof(float));
   return w;
 }
@@ -81,13 +81,18 @@ inline Workspace workspace_layout(const DeviceModel& m, int64_t n) {
 hipError_t launch_articulate(const DeviceModel& m, int64_t n, const float* betas,
                              int64_t betas_stride, const float* pose, const float* trans,
                              float* features, float* transforms, float* features16,
-                             float* tfrag16, float* joints,
+                             float* joints,
                              float* rest_joints, float* rot_mats, hipStream_t stream);
 hipError_t launch_blend(const DeviceModel& m, int64_t n, const float* features,
                         float* vposed, hipStream_t stream);
 hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features16,
-                             const float* tfrag16, const float* trans, float* verts,
+                             const float* transforms, const float* trans, float* verts,
                              float* vposed, hipStream_t stream);
+// The whole forward pass in one launch (articulation fused into blend_skin16).
+hipError_t launch_forward(const DeviceModel& m, int64_t n, const float* betas,
+                          int64_t betas_stride, const float* pose, const float* trans,
+                          float* verts, float* joints, float* vposed, float* rest_joints,
+                          float* rot_mats, hipStream_t stream);
 hipError_t launch_skin(const DeviceModel& m, int64_t n, const float* transforms,
                        const float* vposed, const float* trans, float* verts,
                        hipStream_t stream);

@@ -1,25 +1,25 @@
 // mano_kernels.hip -- gfx950 (MI355X, CDNA4) kernels of the MANO forward pass.
 //
 // Reference hot path: MANOModel.update() in /root/reference/mano_np.py:79-115.
-// It is split into three launches, all on the caller's stream:
+// mano_forward is two launches on the caller's stream:
 //
-//   articulate  one lane per (hand, joint), 32 hands per 512-thread block:
-//               Rodrigues (mano_np.py:117-148) in sinc / half-angle form,
-//               rest joints J = Jreg.T + (Jreg.S).beta (:83, folded in float64
-//               at model load), the 16-joint chain (:96-104) as 3 dependent
-//               levels of wavefront shuffles (5 fingers x depth 3), the
-//               rest-pose removal (:106-110) and the 135 pose features
-//               (R_j - I, :87-91) written straight into MFMA A-fragment tiles.
-//   blend       v_posed = T + [beta | features] . [S ; P]   (:81 and :87-93)
-//               as one K = 145 GEMM on v_mfma_f32_32x32x2_f32.  Each wave keeps
-//               its 32 hands' A fragments in VGPRs for the whole launch; the
-//               4 waves of a block share the basis column tile, staged in LDS by
-//               global_load_lds (LDS-DMA), double-buffered.
-//   skin        LBS (:112-115): one lane per vertex keeps its 16 skinning
-//               weights in VGPRs; the hand's 16 3x4 transforms reach every
-//               lane by DPP row broadcasts (lbs_dpp.h); v_posed streams in and
-//               verts stream out.
-#include "lbs_dpp.h"
+//   articulate    one lane per (hand, joint), 32 hands per 512-thread block:
+//                 Rodrigues (mano_np.py:117-148) in sinc / half-angle form,
+//                 rest joints J = Jreg.T + (Jreg.S).beta (:83, folded in float64
+//                 at model load), the 16-joint chain (:96-104) as 3 dependent
+//                 levels of wavefront shuffles (5 fingers x depth 3), the
+//                 rest-pose removal (:106-110) -> 3x4 transforms, and the 135
+//                 pose features (R_j - I, :87-91) written straight into MFMA
+//                 A-fragment tiles.
+//   blend_skin16  v_posed = [beta | features | 1] . [S ; P ; T] (:81, :87-93) on
+//                 v_mfma_f32_16x16x4_f32 with LDS-DMA-staged basis tiles, then
+//                 LBS (:112-115) with the per-vertex blended transforms also on
+//                 MFMA, v_posed never leaving registers.
+//
+// The staged API adds the unfused kernels: blend (the same GEMM on
+// v_mfma_f32_32x32x2_f32, v_posed to HBM) and skin16 (HBM-streaming LBS with
+// the same MFMA transform tiles as blend_skin16, so both paths agree bit for
+// bit).
 #include "mano_internal.h"
 
 namespace mano {
@@ -36,7 +36,12 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // which has no 0/0 and no 1 - cos cancellation in float32.  Below theta = 1e-2
 // the Taylor series to theta^4 is exact in float32.  Returning R - I (not R)
 // keeps the small pose features of :91 free of the cancellation too.
+//
+// Contraction is off in the articulation helpers: every kernel that inlines
+// them (articulate_kernel, the fused forward) must round identically, so the
+// staged and single-launch paths agree bit for bit; fmaf is spelled out.
 __device__ __forceinline__ void rodrigues_minus_eye(float x, float y, float z, float rm[9]) {
+#pragma clang fp contract(off)
   const float th2 = x * x + y * y + z * z;
   float a, b;
   if (th2 < 1e-4f) {
@@ -60,45 +65,23 @@ __device__ __forceinline__ void rodrigues_minus_eye(float x, float y, float z, f
 }
 
 // ---------------------------------------------------------------------------
-// articulate: 512 threads = 32 hands x 16 joints = exactly one MFMA hand tile.
+// One (hand, joint) lane of the articulation, shared by articulate_kernel and
+// the fused forward kernel.  The 16 lanes of a hand are consecutive
+// (lane & 15 == joint), so the chain's parent transform arrives by shuffle.
+// Out: rm = R_j - I (the pose feature, :91), J = rest joint (:83), t = posed
+// joint = G_j[:3, 3] (:96-104), A = G_j with the rest pose removed (:106-110),
+// row-major 3x4.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(512) void articulate_kernel(
-    const float* __restrict__ betas, int64_t betas_stride, const float* __restrict__ pose,
-    const float* __restrict__ trans, const float* __restrict__ joint_template,
-    const float* __restrict__ joint_shape, const int32_t* __restrict__ parents,
-    const int32_t* __restrict__ depth, int max_depth, int64_t n,
-    float* __restrict__ features, float* __restrict__ transforms,
-    float* __restrict__ features16, float* __restrict__ tfrag16, float* __restrict__ joints,
-    float* __restrict__ rest_joints, float* __restrict__ rot_mats) {
-  __shared__ f32x4 tile[kKGroups * 64];
-  __shared__ f32x4 tile16[2 * kTile16Floats / 4];
-  __shared__ f32x4 ttile16[2 * kTFrag16Floats / 4];
-  float* tilef = reinterpret_cast<float*>(tile);
-  float* tile16f = reinterpret_cast<float*>(tile16);
-  float* ttile16f = reinterpret_cast<float*>(ttile16);
-
-  const int tid = threadIdx.x;
-  const int j = tid & (kJoints - 1);
-  const int hl = tid >> 4;  // hand within the tile
-  const int64_t h = int64_t(blockIdx.x) * kHandTile + hl;
-  const bool valid = h < n;
-
-  float x = 0.f, y = 0.f, z = 0.f;
-  if (valid) {
-    const float* p = pose + h * (kJoints * 3) + 3 * j;
-    x = p[0];
-    y = p[1];
-    z = p[2];
-  }
-  float rm[9];
+__device__ __forceinline__ void articulate_joint(float x, float y, float z,
+                                                 const float (&beta)[kShape], int j, int src,
+                                                 int dep, int max_depth,
+                                                 const float* __restrict__ joint_template,
+                                                 const float* __restrict__ joint_shape,
+                                                 float (&rm)[9], float (&J)[3], float (&t)[3],
+                                                 float (&A)[12]) {
+#pragma clang fp contract(off)
   rodrigues_minus_eye(x, y, z, rm);
-
-  float beta[kShape];
-#pragma unroll
-  for (int s = 0; s < kShape; ++s) beta[s] = valid ? betas[h * betas_stride + s] : 0.f;
-
   // Rest joint of joint j (mano_np.py:83, folded: Jreg.(T + S.beta)).
-  float J[3];
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     float acc = joint_template[j * 3 + c];
@@ -106,23 +89,15 @@ __global__ __launch_bounds__(512) void articulate_kernel(
     for (int s = 0; s < kShape; ++s) acc = fmaf(joint_shape[(j * 3 + c) * kShape + s], beta[s], acc);
     J[c] = acc;
   }
-
   // World rotation / translation, initialised to the root form G_0 = [R_0 | J_0] (:97).
-  float Rw[9], t[3];
+  float Rl[9], Rw[9];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) Rw[i] = rm[i] + ((i % 4 == 0) ? 1.f : 0.f);
+  for (int i = 0; i < 9; ++i) Rl[i] = Rw[i] = rm[i] + ((i % 4 == 0) ? 1.f : 0.f);
   t[0] = J[0];
   t[1] = J[1];
   t[2] = J[2];
-  float Rl[9];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) Rl[i] = Rw[i];
-
   // Chain (:98-104): G_j = G_parent . [R_j | J_j - J_parent], one tree level per
   // iteration; the parent's finished transform arrives by a wavefront shuffle.
-  const int par = parents[j];
-  const int dep = depth[j];
-  const int src = ((tid & 63) & ~(kJoints - 1)) + (par < 0 ? 0 : par);
   for (int d = 1; d <= max_depth; ++d) {
     float pR[9], pt[3], pJ[3];
 #pragma unroll
@@ -144,59 +119,103 @@ __global__ __launch_bounds__(512) void articulate_kernel(
       }
     }
   }
-
   // Skinning transform A_j = [Rw | t - Rw J] (rest-pose removal, :106-110).
-  float Aj[12];
 #pragma unroll
   for (int r = 0; r < 3; ++r) {
-    Aj[r * 4 + 0] = Rw[r * 3 + 0];
-    Aj[r * 4 + 1] = Rw[r * 3 + 1];
-    Aj[r * 4 + 2] = Rw[r * 3 + 2];
-    Aj[r * 4 + 3] = t[r] - (Rw[r * 3 + 0] * J[0] + Rw[r * 3 + 1] * J[1] + Rw[r * 3 + 2] * J[2]);
+    A[r * 4 + 0] = Rw[r * 3 + 0];
+    A[r * 4 + 1] = Rw[r * 3 + 1];
+    A[r * 4 + 2] = Rw[r * 3 + 2];
+    A[r * 4 + 3] = t[r] - (Rw[r * 3 + 0] * J[0] + Rw[r * 3 + 1] * J[1] + Rw[r * 3 + 2] * J[2]);
   }
-  // ... and in the fused kernel's MFMA A-fragment layout (mano_internal.h):
-  // hand (hl & 15) of 16-hand tile (hl >> 4), joint j = 4 s + (lane >> 4).
-  {
-    const int ln16 = (hl & 15) + 16 * (j & 3);
-    float* t16 = ttile16f + (hl >> 4) * kTFrag16Floats;
+}
+
+// Optional per-joint outputs of a valid lane: posed joints (+ trans), rest
+// joints, local rotations R_j = I + rm.
+__device__ __forceinline__ void store_joint_outputs(int64_t h, int j, const float* __restrict__ trans,
+                                                    const float (&rm)[9], const float (&J)[3],
+                                                    const float (&t)[3], float* __restrict__ joints,
+                                                    float* __restrict__ rest_joints,
+                                                    float* __restrict__ rot_mats) {
+  if (joints) {
+    float* o = joints + h * (kJoints * 3) + 3 * j;
 #pragma unroll
-    for (int ck = 0; ck < 12; ++ck) t16[(ck * 64 + ln16) * 4 + (j >> 2)] = Aj[ck];
+    for (int c = 0; c < 3; ++c) o[c] = t[c] + (trans ? trans[h * 3 + c] : 0.f);
   }
+  if (rest_joints) {
+    float* o = rest_joints + h * (kJoints * 3) + 3 * j;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) o[c] = J[c];
+  }
+  if (rot_mats) {
+    float* o = rot_mats + h * (kJoints * 9) + 9 * j;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) o[i] = rm[i] + ((i % 4 == 0) ? 1.f : 0.f);
+  }
+}
+
+// Element k of hand row `hl` (0..15) of the blend GEMM A operand X in the
+// 16x16x4 fragment layout: step s = k / 4, lane hl + 16 (k & 3), packed as
+// [s / 4][64 lanes][s % 4] (mano_internal.h).
+__device__ __forceinline__ int x16_index(int hl, int k) {
+  const int s = k >> 2;
+  return (((s >> 2) * 64) + hl + 16 * (k & 3)) * 4 + (s & 3);
+}
+
+// ---------------------------------------------------------------------------
+// articulate: 512 threads = 32 hands x 16 joints = exactly one MFMA hand tile.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(512) void articulate_kernel(
+    const float* __restrict__ betas, int64_t betas_stride, const float* __restrict__ pose,
+    const float* __restrict__ trans, const float* __restrict__ joint_template,
+    const float* __restrict__ joint_shape, const int32_t* __restrict__ parents,
+    const int32_t* __restrict__ depth, int max_depth, int64_t n,
+    float* __restrict__ features, float* __restrict__ transforms,
+    float* __restrict__ features16, float* __restrict__ joints,
+    float* __restrict__ rest_joints, float* __restrict__ rot_mats) {
+  __shared__ f32x4 tile[kKGroups * 64];
+  __shared__ f32x4 tile16[2 * kTile16Floats / 4];
+  float* tilef = reinterpret_cast<float*>(tile);
+  float* tile16f = reinterpret_cast<float*>(tile16);
+
+  const int tid = threadIdx.x;
+  const int j = tid & (kJoints - 1);
+  const int hl = tid >> 4;  // hand within the tile
+  const int64_t h = int64_t(blockIdx.x) * kHandTile + hl;
+  const bool valid = h < n;
+
+  float x = 0.f, y = 0.f, z = 0.f;
+  if (valid) {
+    const float* p = pose + h * (kJoints * 3) + 3 * j;
+    x = p[0];
+    y = p[1];
+    z = p[2];
+  }
+  float beta[kShape];
+#pragma unroll
+  for (int s = 0; s < kShape; ++s) beta[s] = valid ? betas[h * betas_stride + s] : 0.f;
+  const int par = parents[j];
+  const int src = ((tid & 63) & ~(kJoints - 1)) + (par < 0 ? 0 : par);
+  float rm[9], J[3], t[3], Aj[12];
+  articulate_joint(x, y, z, beta, j, src, depth[j], max_depth, joint_template, joint_shape, rm, J,
+                   t, Aj);
   if (valid) {
     float* A = transforms + h * kTransformFloats + j * 12;
 #pragma unroll
     for (int m = 0; m < 12; ++m) A[m] = Aj[m];
-    if (joints) {
-      float* o = joints + h * (kJoints * 3) + 3 * j;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) o[c] = t[c] + (trans ? trans[h * 3 + c] : 0.f);
-    }
-    if (rest_joints) {
-      float* o = rest_joints + h * (kJoints * 3) + 3 * j;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) o[c] = J[c];
-    }
-    if (rot_mats) {
-      float* o = rot_mats + h * (kJoints * 9) + 9 * j;
-#pragma unroll
-      for (int i = 0; i < 9; ++i) o[i] = Rl[i];
-    }
+    store_joint_outputs(h, j, trans, rm, J, t, joints, rest_joints, rot_mats);
   }
 
   // Blend-GEMM A operand: X[h][k], k < 10 beta, 10 <= k < 145 features
   // (k = 10 + 9(j-1) + 3 row + col, the ravel order of :91), X[h][145] = 1
-  // (selects the template row of the basis), zeros up to 152.
-  // Fragment layout for v_mfma_f32_32x32x2_f32: step s = k/2 holds
-  // X[hand = lane & 31][k = 2s + (lane >> 5)]; 4 steps packed per float4.
+  // (selects the template row of the basis), zeros up to the padded K.
+  // 32x32x2 layout (blend kernel): step s = k/2 holds X[hand = lane & 31][k =
+  // 2s + (lane >> 5)], 4 steps per float4; 16x16x4 layout: x16_index.
   float* t16 = tile16f + (hl >> 4) * kTile16Floats;
   auto put = [&](int k, float v) {
     const int s = k >> 1;
     const int ln = hl + 32 * (k & 1);
     if (k < kKGroups * 8) tilef[(((s >> 2) * 64) + ln) * 4 + (s & 3)] = v;
-    if (k < kGroups16 * 16) {  // 16x16x4 fragments: step s16 = k / 4, lane (hl & 15) + 16 (k & 3)
-      const int s16 = k >> 2;
-      t16[(((s16 >> 2) * 64) + (hl & 15) + 16 * (k & 3)) * 4 + (s16 & 3)] = v;
-    }
+    if (k < kGroups16 * 16) t16[x16_index(hl & 15, k)] = v;
   };
   if (j == 0) {
 #pragma unroll
@@ -213,8 +232,6 @@ __global__ __launch_bounds__(512) void articulate_kernel(
   for (int i = tid; i < kKGroups * 64; i += 512) dst[i] = tile[i];
   f32x4* d16 = reinterpret_cast<f32x4*>(features16 + int64_t(blockIdx.x) * 2 * kTile16Floats);
   for (int i = tid; i < 2 * kTile16Floats / 4; i += 512) d16[i] = tile16[i];
-  f32x4* t16d = reinterpret_cast<f32x4*>(tfrag16 + int64_t(blockIdx.x) * 2 * kTFrag16Floats);
-  for (int i = tid; i < 2 * kTFrag16Floats / 4; i += 512) t16d[i] = ttile16[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -344,110 +361,295 @@ __device__ __forceinline__ f32x4 mfma16_tile(const float (&a)[kGroups16 * 4],
   return acc;
 }
 
-template <bool kTrans>
-__global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
-    const float* __restrict__ features16, const float* __restrict__ basis16,
-    const float* __restrict__ wfrag16, const float* __restrict__ tfrag16,
-    const float* __restrict__ trans, float* __restrict__ verts, float* __restrict__ vposed,
-    int64_t n, int n_verts, int n_groups) {
-  __shared__ f32x4 bs[2][kGroups16 * 64];  // basis tile ring 2 x 10 KB
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t nt16 = (n + 15) / 16;
-  const int64_t t16 = int64_t(blockIdx.x) * 4 + wave;
-  const bool active = t16 < nt16;
-  const int64_t tc = active ? t16 : nt16 - 1;
-  const int64_t h0 = tc * 16;
-  const int row0 = 4 * (lane >> 4);  // D rows (hands) of this lane: row0 + r
-  const int col = lane & 15;         // D column (vertex of the group)
-
-  float a[kGroups16 * 4];
-  {
-    const f32x4* src = reinterpret_cast<const f32x4*>(features16 + tc * kTile16Floats) + lane;
+// LBS A fragments of a 16-hand tile straight from the [n][16][3][4]
+// transforms: F[c * 4 + k][q] = A_j(hand h0 + (lane & 15))[c][k], joint
+// j = 4 q + (lane >> 4) (rows past the batch end repeat the last hand).
+__device__ __forceinline__ void load_lbs_frags(const float* __restrict__ transforms, int64_t h0,
+                                               int64_t n, int lane, float (&F)[12][4]) {
+  const int64_t n_left = n - 1 - h0;  // >= 0
+  const int hl = min(lane & 15, int(n_left < 15 ? n_left : 15));
+  const f32x4* A = reinterpret_cast<const f32x4*>(transforms + h0 * kTransformFloats) +
+                   (hl * kTransformFloats + (lane >> 4) * 12) / 4;
 #pragma unroll
-    for (int g = 0; g < kGroups16; ++g) {
-      const f32x4 v = src[g * 64];
-      a[4 * g + 0] = v[0];
-      a[4 * g + 1] = v[1];
-      a[4 * g + 2] = v[2];
-      a[4 * g + 3] = v[3];
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const f32x4 v = A[q * 12 + i];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) F[4 * i + e][q] = v[e];
     }
   }
-  f32x4 F[12];  // LBS A fragments, tile (c, k) = c * 4 + k, resident for all groups
-  {
-    const f32x4* src = reinterpret_cast<const f32x4*>(tfrag16 + tc * kTFrag16Floats) + lane;
-#pragma unroll
-    for (int i = 0; i < 12; ++i) F[i] = src[i * 64];
-  }
-  __shared__ float trs[4][16 * 3];  // the wave's 16 translations, read back at the stores
-  if constexpr (kTrans) {
-    if (lane < 48) {
-      const int64_t h = h0 + lane / 3;
-      trs[wave][lane] = trans[(h < n ? h : n - 1) * 3 + lane % 3];
-    }
-  }
-  const int vstride32 = 3 * n_verts;
-  const int64_t n_left = n - h0;
-  const int n_valid = active ? (n_left < 16 ? int(n_left) : 16) : 0;
-  float* vtile = verts + h0 * int64_t(vstride32);
-  float* ptile = vposed ? vposed + h0 * int64_t(vstride32) : nullptr;
-  const int n_tiles = 3 * n_groups;
+}
 
-  stage_basis_tile16(basis16, 0, bs[0], wave, lane);
-  __syncthreads();
-
-  for (int grp = 0; grp < n_groups; ++grp) {
-    const f32x4 wf = reinterpret_cast<const f32x4*>(wfrag16 + int64_t(grp) * kWFrag16Floats)[lane];
-    f32x4 p[3];
+// LBS of one 16-hand x 16-vertex tile (mano_np.py:112-115): the 12 transform
+// tiles T_{c,k} = F_{c,k} . W^T (4 MFMAs each, K = 16 joints) applied to the
+// rest vertices p[coord] as out_c = T_c3 + T_c2 z + T_c1 y + T_c0 x (fmaf,
+// translation column first).  kFence pins the three coordinate rows in order
+// so at most 16 T registers are live (hipcc otherwise hoists all 48 MFMAs).
+template <bool kFence = false>
+__device__ __forceinline__ void lbs_apply16(const float (&F)[12][4], const f32x4& wf,
+                                            const f32x4 (&p)[3], f32x4 (&out)[3]) {
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const int t = 3 * grp + q;
-      if (t + 1 < n_tiles) stage_basis_tile16(basis16, t + 1, bs[(t + 1) & 1], wave, lane);
-      p[q] = mfma16_tile(a, bs[t & 1], lane);
-      __syncthreads();
-    }
-    int vb = grp * 16;
-    if (vb > n_verts - 16) vb = n_verts - 16;
-    const int voff = 3 * (vb + col);
-    f32x4 out[3];
+  for (int c = 0; c < 3; ++c) {
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
+    for (int kk = 0; kk < 4; ++kk) {
+      const int k = 3 - kk;
+      const float* f = F[c * 4 + k];
+      f32x4 T = {};
+      T = __builtin_amdgcn_mfma_f32_16x16x4f32(f[0], wf[0], T, 0, 0, 0);
+      T = __builtin_amdgcn_mfma_f32_16x16x4f32(f[1], wf[1], T, 0, 0, 0);
+      T = __builtin_amdgcn_mfma_f32_16x16x4f32(f[2], wf[2], T, 0, 0, 0);
+      T = __builtin_amdgcn_mfma_f32_16x16x4f32(f[3], wf[3], T, 0, 0, 0);
+      if (k == 3) {
+        out[c] = T;
+      } else {
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const int k = 3 - kk;  // translation column first, as in the skin kernel
-        const f32x4 f = F[c * 4 + k];
-        f32x4 T = {};
-        T = __builtin_amdgcn_mfma_f32_16x16x4f32(f[0], wf[0], T, 0, 0, 0);
-        T = __builtin_amdgcn_mfma_f32_16x16x4f32(f[1], wf[1], T, 0, 0, 0);
-        T = __builtin_amdgcn_mfma_f32_16x16x4f32(f[2], wf[2], T, 0, 0, 0);
-        T = __builtin_amdgcn_mfma_f32_16x16x4f32(f[3], wf[3], T, 0, 0, 0);
-        if (k == 3) {
-          out[c] = T;
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) out[c][r] = fmaf(T[r], p[k][r], out[c][r]);
-        }
+        for (int r = 0; r < 4; ++r) out[c][r] = fmaf(T[r], p[k][r], out[c][r]);
       }
+    }
+    if constexpr (kFence) {
+      asm volatile("" : "+v"(out[c]));  // materialise row c here (no SLP across rows)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// lbs_apply16 for rest vertices held as per-row points p[r] = (x, y, z) of
+// hand row0 + r (the skin kernel's loads); same fmaf order.  Each coordinate
+// row is materialised before the next so at most 16 T registers are live.
+typedef float f32x3 __attribute__((ext_vector_type(3)));
+__device__ __forceinline__ void lbs_apply16_rows(const float (&F)[12][4], const f32x4& wf,
+                                                 const f32x3 (&p)[4], f32x4 (&out)[3]) {
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    f32x4 T[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float* f = F[c * 4 + k];
+      T[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(f[0], wf[0], f32x4{}, 0, 0, 0);
+      T[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(f[1], wf[1], T[k], 0, 0, 0);
+      T[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(f[2], wf[2], T[k], 0, 0, 0);
+      T[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(f[3], wf[3], T[k], 0, 0, 0);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int hr = row0 + r;
-      if (hr < n_valid) {
-        float o0 = out[0][r], o1 = out[1][r], o2 = out[2][r];
-        if constexpr (kTrans) {
-          o0 += trs[wave][hr * 3 + 0];
-          o1 += trs[wave][hr * 3 + 1];
-          o2 += trs[wave][hr * 3 + 2];
+      float o = T[3][r];
+      o = fmaf(T[2][r], p[r][2], o);
+      o = fmaf(T[1][r], p[r][1], o);
+      o = fmaf(T[0][r], p[r][0], o);
+      asm volatile("" : "+v"(o));  // one scalar chain per row (no SLP pairing)
+      out[c][r] = o;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// Inputs of the articulation when the fused kernel computes it itself.
+struct ArticulateArgs {
+  const float* betas;
+  int64_t betas_stride;
+  const float* pose;
+  const float* joint_template;
+  const float* joint_shape;
+  const int32_t* parents;
+  const int32_t* depth;
+  int max_depth;
+  float* joints;
+  float* rest_joints;
+  float* rot_mats;
+};
+
+// Work split of the persistent launches: the (tile, vertex group) units are
+// cut into gridDim.x (blend_skin16: one range per block of 4 hand tiles) or
+// 4 gridDim.x (skin16: one range per wave) equal contiguous ranges, with the
+// grid sized to the resident capacity of the chip, so every SIMD gets the same
+// MFMA / HBM work and there is no partially-filled second wave of blocks.
+__device__ __forceinline__ void unit_range(int64_t units, int64_t worker, int64_t n_workers,
+                                           int64_t& begin, int64_t& end) {
+  begin = worker * units / n_workers;
+  end = (worker + 1) * units / n_workers;
+}
+
+// kArticulate: the whole forward pass in one launch.  Each wave first
+// articulates its own 16 hands (4 passes of 4 hands x 16 joint lanes, the same
+// articulate_joint as articulate_kernel) and hands the results to its GEMM /
+// LBS lanes through a 12-KB LDS staging area -- first the features in
+// A-fragment order, then the transforms in LBS fragment order -- which the
+// basis tile ring re-uses afterwards.  Otherwise the A fragments and transforms are
+// read from the workspace written by articulate_kernel.
+//
+// A block owns a contiguous range of (quad of 4 hand tiles, vertex group)
+// units; at each quad it (re)builds its waves' operands, then runs that
+// quad's groups: 3 GEMM tiles (x, y, z) per group with the basis tiles staged
+// in LDS by LDS-DMA one tile ahead, then the LBS epilogue.
+template <bool kTrans, bool kArticulate>
+__global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
+    const float* __restrict__ features16, const float* __restrict__ transforms,
+    ArticulateArgs art, const float* __restrict__ basis16, const float* __restrict__ wfrag16,
+    const float* __restrict__ trans, float* __restrict__ verts, float* __restrict__ vposed,
+    int64_t n, int n_verts, int n_groups) {
+  constexpr int kStageF4 = 12 * 64;          // 12 KB of staging per wave
+  constexpr int kRingF4 = kGroups16 * 64;    // one basis tile, 10 KB; ring of 2 at lds[0]
+  __shared__ f32x4 lds[kArticulate ? 4 * kStageF4 : 2 * kRingF4];
+  __shared__ float trs[4][16 * 3];  // the wave's 16 translations, read back at the stores
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int vstride32 = 3 * n_verts;
+  const int64_t nt16 = (n + 15) / 16;
+  const int64_t n_quads = (nt16 + 3) / 4;
+  int64_t u, u_end;
+  unit_range(n_quads * n_groups, blockIdx.x, gridDim.x, u, u_end);
+
+  while (u < u_end) {
+    const int64_t quad = u / n_groups;
+    const int g0 = int(u - quad * n_groups);
+    const int g1 = int(n_groups - g0 < u_end - u ? n_groups : g0 + (u_end - u));
+    u += g1 - g0;
+    const int64_t t16 = quad * 4 + wave;
+    const bool active = t16 < nt16;
+    const int64_t tc = active ? t16 : nt16 - 1;
+    const int64_t h0 = tc * 16;
+    const int n_valid = active ? int(n - h0 < 16 ? n - h0 : 16) : 0;
+
+    // An opaque lane index per range: keeps hipcc from hoisting lane-dependent
+    // addresses and loads (the 33 joint constants per lane, the staging
+    // offsets) out of the range loop, which would hold them in registers --
+    // spilled -- across the GEMM.
+    int lane = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane));
+    const int row0 = 4 * (lane >> 4);  // D rows (hands) of this lane: row0 + r
+    const int col = lane & 15;         // D column (vertex of the group)
+    const float* jt = art.joint_template;
+    const float* js = art.joint_shape;
+    const int32_t* parents = art.parents;
+    const int32_t* depth = art.depth;
+
+    float a[kGroups16 * 4];
+    float F[12][4];  // LBS A fragments, tile (c, k) = c * 4 + k, resident for the quad
+    if constexpr (kArticulate) {
+      // (Every ring read of the previous range ended before its last barrier.)
+      float* stg = reinterpret_cast<float*>(lds + wave * kStageF4);
+      const f32x4* stg4 = lds + wave * kStageF4;
+      const int j = lane & 15;
+      const int par = parents[j];
+      const int dep = depth[j];
+      const int src = (lane & ~15) + (par < 0 ? 0 : par);
+      const int n_last = int(n - h0 < 16 ? n - h0 : 16) - 1;  // rows past the end repeat it
+      // All of the prologue's global loads first (one latency, not four).
+      float xyz[4][3], beta[4][kShape];
+#pragma unroll
+      for (int ps = 0; ps < 4; ++ps) {
+        const int64_t h = h0 + min(4 * ps + (lane >> 4), n_last);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) xyz[ps][c] = art.pose[h * (kJoints * 3) + 3 * j + c];
+#pragma unroll
+        for (int q = 0; q < kShape; ++q) beta[ps][q] = art.betas[h * art.betas_stride + q];
+      }
+      // Pass ps: lanes (hand 4 ps + (lane >> 4), joint lane & 15).  The
+      // features go to the staging area in A-fragment order right away; the
+      // transforms wait in registers until the features have been read back.
+      float Aj[4][12];
+#pragma unroll
+      for (int ps = 0; ps < 4; ++ps) {
+        const int hl = 4 * ps + (lane >> 4);
+        float rm[9], J[3], t[3];
+        articulate_joint(xyz[ps][0], xyz[ps][1], xyz[ps][2], beta[ps], j, src, dep, art.max_depth,
+                         jt, js, rm, J, t, Aj[ps]);
+        if (j == 0) {
+#pragma unroll
+          for (int q = 0; q < kShape; ++q) stg[x16_index(hl, q)] = beta[ps][q];
+          stg[x16_index(hl, kK)] = 1.f;  // X[:, 145] = 1 selects the template row
+#pragma unroll
+          for (int k = kK + 1; k < kGroups16 * 16; ++k) stg[x16_index(hl, k)] = 0.f;
+        } else {
+#pragma unroll
+          for (int m = 0; m < 9; ++m) stg[x16_index(hl, kShape + 9 * (j - 1) + m)] = rm[m];
         }
-        float* o = vtile + unsigned(hr * vstride32 + voff);
-        o[0] = o0;
-        o[1] = o1;
-        o[2] = o2;
-        if (ptile) {
-          float* pv = ptile + unsigned(hr * vstride32 + voff);
-          pv[0] = p[0][r];
-          pv[1] = p[1][r];
-          pv[2] = p[2][r];
+        if (g0 == 0 && hl < n_valid)  // the joint outputs come from the range holding group 0
+          store_joint_outputs(h0 + hl, j, trans, rm, J, t, art.joints, art.rest_joints,
+                              art.rot_mats);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int g = 0; g < kGroups16; ++g) {
+        const f32x4 v = stg4[g * 64 + lane];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[4 * g + q] = v[q];
+      }
+      __syncthreads();
+      // LBS fragment order: F_{c,k}[q] of lane L = A_{4q + (L >> 4)}(hand L & 15)[c][k].
+#pragma unroll
+      for (int ps = 0; ps < 4; ++ps) {
+        const int hl = 4 * ps + (lane >> 4);
+#pragma unroll
+        for (int ck = 0; ck < 12; ++ck)
+          stg[(ck * 64 + hl + 16 * (j & 3)) * 4 + (j >> 2)] = Aj[ps][ck];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int ck = 0; ck < 12; ++ck) {
+        const f32x4 v = stg4[ck * 64 + lane];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) F[ck][q] = v[q];
+      }
+      __syncthreads();  // the basis ring overwrites the staging areas next
+    } else {
+      const f32x4* src = reinterpret_cast<const f32x4*>(features16 + tc * kTile16Floats) + lane;
+#pragma unroll
+      for (int g = 0; g < kGroups16; ++g) {
+        const f32x4 v = src[g * 64];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[4 * g + q] = v[q];
+      }
+      load_lbs_frags(transforms, h0, n, lane, F);
+    }
+    if constexpr (kTrans) {
+      if (lane < 48) {
+        const int64_t h = h0 + lane / 3;
+        trs[wave][lane] = trans[(h < n ? h : n - 1) * 3 + lane % 3];
+      }
+    }
+    float* vtile = verts + h0 * int64_t(vstride32);
+    float* ptile = vposed ? vposed + h0 * int64_t(vstride32) : nullptr;
+    const int t_end = 3 * g1;
+
+    stage_basis_tile16(basis16, 3 * g0, lds + ((3 * g0) & 1) * kRingF4, wave, lane);
+    __syncthreads();
+
+    for (int grp = g0; grp < g1; ++grp) {
+      const f32x4 wf = reinterpret_cast<const f32x4*>(wfrag16 + int64_t(grp) * kWFrag16Floats)[lane];
+      f32x4 p[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int t = 3 * grp + q;
+        if (t + 1 < t_end) stage_basis_tile16(basis16, t + 1, lds + ((t + 1) & 1) * kRingF4, wave, lane);
+        p[q] = mfma16_tile(a, lds + (t & 1) * kRingF4, lane);
+        __syncthreads();
+      }
+      int vb = grp * 16;
+      if (vb > n_verts - 16) vb = n_verts - 16;
+      const int voff = 3 * (vb + col);
+      f32x4 out[3];
+      lbs_apply16(F, wf, p, out);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int hr = row0 + r;
+        if (hr < n_valid) {
+          float o0 = out[0][r], o1 = out[1][r], o2 = out[2][r];
+          if constexpr (kTrans) {
+            o0 += trs[wave][hr * 3 + 0];
+            o1 += trs[wave][hr * 3 + 1];
+            o2 += trs[wave][hr * 3 + 2];
+          }
+          float* o = vtile + unsigned(hr * vstride32 + voff);
+          o[0] = o0;
+          o[1] = o1;
+          o[2] = o2;
+          if (ptile) {
+            float* pv = ptile + unsigned(hr * vstride32 + voff);
+            pv[0] = p[0][r];
+            pv[1] = p[1][r];
+            pv[2] = p[2][r];
+          }
         }
       }
     }
@@ -455,77 +657,99 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// skin: lane = vertex, wave = run of kSkinHands hands; grid (hand runs, vertex groups).
+// skin16: standalone LBS (mano_np.py:112-115) over a v_posed buffer, HBM
+// streaming.  Each wave owns a contiguous range of (16-hand tile, 16-vertex
+// group) units; per tile it loads the transform fragments into VGPRs, then
+// per group computes the same 12 v_mfma_f32_16x16x4_f32 transform tiles as
+// blend_skin16 (so both paths agree bit for bit) and applies them to v_posed,
+// which is prefetched kDepth groups ahead in a register ring (2 waves per SIMD
+// with ~18 KB of loads in flight each: HBM latency needs the bytes in flight
+// more than the extra waves).
 // ---------------------------------------------------------------------------
-constexpr int kSkinHands = 16;
-
-__global__ __launch_bounds__(256) void skin_kernel(
-    const float* __restrict__ weights, const float* __restrict__ transforms,
-    const float* __restrict__ vposed, const float* __restrict__ trans, int trans_stride,
-    float* __restrict__ verts, int64_t n, int n_verts) {
+template <bool kTrans, int kDepth>
+__global__ __launch_bounds__(256, 2) void skin16_kernel(
+    const float* __restrict__ transforms, const float* __restrict__ wfrag16,
+    const float* __restrict__ vposed, const float* __restrict__ trans,
+    float* __restrict__ verts, int64_t n, int n_verts, int n_groups) {
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // No lane is ever masked: the last vertex group is shifted back to end at
-  // vertex V-1 (it re-computes, and re-writes with identical values, a few
-  // vertices of the previous group), and an odd tail hand is processed twice.
-  // Branch-free bodies keep hipcc from sinking the blend into a store branch
-  // or waiting vmcnt(0) at control-flow joins.
-  int vbase = int(blockIdx.y) * 64;
-  if (vbase > n_verts - 64) vbase = n_verts - 64;
-  if (vbase < 0) vbase = 0;
-  const int v = min(vbase + lane, n_verts - 1);
-  float w[kJoints];
-  {
-    const f32x4* wp = reinterpret_cast<const f32x4*>(weights + int64_t(v) * kJoints);
+  const int row0 = 4 * (lane >> 4);
+  const int col = lane & 15;
+  const int vstride = 3 * n_verts;
+  const int64_t nt16 = (n + 15) / 16;
+  int64_t u, u_end;
+  unit_range(nt16 * n_groups, int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6), int64_t(gridDim.x) * 4,
+             u, u_end);
+  auto vbase = [&](int grp) { return 3 * min(grp * 16, n_verts - 16); };
+
+  while (u < u_end) {  // no barriers: each wave runs its own range
+    const int64_t tile = u / n_groups;
+    const int g0 = int(u - tile * n_groups);
+    const int g1 = int(n_groups - g0 < u_end - u ? n_groups : g0 + (u_end - u));
+    u += g1 - g0;
+    const int64_t h0 = tile * 16;
+    const int n_valid = int(n - h0 < 16 ? n - h0 : 16);
+
+    float F[12][4];
+    load_lbs_frags(transforms, h0, n, lane, F);
+    float tr[4][3] = {};
+    if constexpr (kTrans) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const f32x4 q = wp[i];
-      w[4 * i + 0] = q[0];
-      w[4 * i + 1] = q[1];
-      w[4 * i + 2] = q[2];
-      w[4 * i + 3] = q[3];
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) tr[r][c] = trans[(h0 + min(row0 + r, n_valid - 1)) * 3 + c];
     }
-  }
-  const int64_t h0 = (int64_t(blockIdx.x) * 4 + wave) * kSkinHands;
-  if (h0 >= n) return;
-  const int cnt = int(n - h0 < kSkinHands ? n - h0 : kSkinHands);  // hands of this wave
-  const int64_t stride = int64_t(n_verts) * 3;
-  const float* vrow = vposed + h0 * stride + 3 * v;
-  float* orow = verts + h0 * stride + 3 * v;
-  const float* Abase = transforms + h0 * kTransformFloats;
-  // v_posed rows and transforms ping-pong: each buffer is re-loaded (two
-  // hands ahead) right after it is consumed, so no register rotation waits on
-  // a fresh load and ~2 hands of loads stay in flight per wave.
-  float P[2][3], AJ[2][12];
+    // Per-lane row offsets (rows past the batch end re-read the last hand).
+    int roff[4];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int k = min(u, cnt - 1);
-    const float* q = vrow + int64_t(k) * stride;
-    P[u][0] = q[0];
-    P[u][1] = q[1];
-    P[u][2] = q[2];
-    lbs_load_joint_row(Abase + k * kTransformFloats, lane, AJ[u]);
-  }
-  for (int i = 0; i < cnt; i += 2) {
+    for (int r = 0; r < 4; ++r) roff[r] = min(row0 + r, n_valid - 1) * vstride + 3 * col;
+    const float* ptile = vposed + h0 * int64_t(vstride);
+    float* vtile = verts + h0 * int64_t(vstride);
+    // Group g's operands (rest vertices and the W fragment) are loaded kDepth
+    // groups ahead, so the wait before group g's MFMAs only covers loads that
+    // were issued kDepth - 1 groups earlier.  Each row's point is one dwordx3
+    // load kept as loaded (a register shuffle would wait on the prefetch).
+    auto load_p = [&](int grp, f32x3 (&p)[4], f32x4& wf) {
+      const int g = min(grp, g1 - 1);
+      const float* src = ptile + vbase(g);
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int k = min(i + u, cnt - 1);
-      float T[12];
-      lbs_blend16(T, AJ[u], w);
-      const float* tp = trans + (h0 + k) * trans_stride;  // stride 0: a zero vector
-      const float t0 = tp[0], t1 = tp[1], t2 = tp[2];
-      const float p0 = P[u][0], p1 = P[u][1], p2 = P[u][2];
-      const int kn = min(i + u + 2, cnt - 1);
-      const float* q = vrow + int64_t(kn) * stride;
-      P[u][0] = q[0];
-      P[u][1] = q[1];
-      P[u][2] = q[2];
-      lbs_load_joint_row(Abase + kn * kTransformFloats, lane, AJ[u]);
-      float* o = orow + int64_t(k) * stride;
-      o[0] = fmaf(T[0], p0, fmaf(T[1], p1, fmaf(T[2], p2, T[3]))) + t0;
-      o[1] = fmaf(T[4], p0, fmaf(T[5], p1, fmaf(T[6], p2, T[7]))) + t1;
-      o[2] = fmaf(T[8], p0, fmaf(T[9], p1, fmaf(T[10], p2, T[11]))) + t2;
+      for (int r = 0; r < 4; ++r) p[r] = *reinterpret_cast<const f32x3*>(src + roff[r]);
+      wf = reinterpret_cast<const f32x4*>(wfrag16 + int64_t(g) * kWFrag16Floats)[lane];
+    };
+    // Ring of kDepth register buffers: group g lives in slot g % kDepth and is
+    // re-loaded with group g + kDepth right after it is consumed.
+    f32x3 P[kDepth][4];
+    f32x4 W[kDepth];
+#pragma unroll
+    for (int d = 0; d < kDepth; ++d) load_p(g0 + d, P[d], W[d]);
+    auto body = [&](int grp, f32x3 (&p)[4], f32x4& wf) {
+      f32x4 out[3];
+      lbs_apply16_rows(F, wf, p, out);
+      load_p(grp + kDepth, p, wf);
+      // Branch-free stores: a row past the batch end holds the last hand's
+      // values and re-writes them (identical bits) to that hand's address.
+      const int vb = vbase(grp);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float* o = vtile + unsigned(roff[r] + vb);
+        float o0 = out[0][r], o1 = out[1][r], o2 = out[2][r];
+        if constexpr (kTrans) {
+          o0 += tr[r][0];
+          o1 += tr[r][1];
+          o2 += tr[r][2];
+        }
+        o[0] = o0;
+        o[1] = o1;
+        o[2] = o2;
+      }
+    };
+    int grp = g0;
+    for (; grp + kDepth <= g1; grp += kDepth) {
+#pragma unroll
+      for (int d = 0; d < kDepth; ++d) body(grp + d, P[d], W[d]);
     }
+#pragma unroll
+    for (int d = 0; d < kDepth; ++d)
+      if (grp + d < g1) body(grp + d, P[d], W[d]);
   }
 }
 
@@ -568,12 +792,12 @@ __global__ __launch_bounds__(256) void rodrigues_kernel(const float* __restrict_
 hipError_t launch_articulate(const DeviceModel& m, int64_t n, const float* betas,
                              int64_t betas_stride, const float* pose, const float* trans,
                              float* features, float* transforms, float* features16,
-                             float* tfrag16, float* joints,
+                             float* joints,
                              float* rest_joints, float* rot_mats, hipStream_t stream) {
   const int64_t blocks = (n + kHandTile - 1) / kHandTile;
   hipLaunchKernelGGL(articulate_kernel, dim3(unsigned(blocks)), dim3(512), 0, stream, betas,
                      betas_stride, pose, trans, m.joint_template, m.joint_shape, m.parents,
-                     m.depth, m.max_depth, n, features, transforms, features16, tfrag16, joints,
+                     m.depth, m.max_depth, n, features, transforms, features16, joints,
                      rest_joints, rot_mats);
   return hipGetLastError();
 }
@@ -587,28 +811,88 @@ hipError_t launch_blend(const DeviceModel& m, int64_t n, const float* features, 
   return hipGetLastError();
 }
 
-hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features16,
-                             const float* tfrag16, const float* trans, float* verts,
-                             float* vposed, hipStream_t stream) {
-  const int64_t nt16 = (n + 15) / 16;
-  const dim3 grid{unsigned((nt16 + 3) / 4)}, block{256u};
-  if (trans)
-    hipLaunchKernelGGL(blend_skin16_kernel<true>, grid, block, 0, stream, features16, m.basis16,
-                       m.wfrag16, tfrag16, trans, verts, vposed, n, m.n_verts, m.n_groups16);
-  else
-    hipLaunchKernelGGL(blend_skin16_kernel<false>, grid, block, 0, stream, features16, m.basis16,
-                       m.wfrag16, tfrag16, trans, verts, vposed, n, m.n_verts, m.n_groups16);
+namespace {
+
+// Blocks of `kernel` (256 threads) the device holds at once.  Each persistent
+// kernel states the blocks per CU it is built for (its __launch_bounds__); the
+// occupancy API only caps that, because it reads one block per CU high for
+// kernels using 97-112 SGPRs on gfx950 (MI355X_MICROARCH.md, correctness
+// boundaries) -- the fused forward uses 106.
+constexpr int kBlendSkinBlocksPerCU = 3;  // 168 VGPRs
+constexpr int kSkinBlocksPerCU = 2;       // <= 256 VGPRs
+constexpr int kSkinDepth = 6;             // skin16 prefetch depth (groups)
+
+template <class Kernel>
+int64_t resident_blocks(Kernel kernel, const DeviceModel& m, int design_per_cu) {
+  int b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, 256, 0) != hipSuccess || b < 1) b = 1;
+  if (b > design_per_cu) b = design_per_cu;
+  return int64_t(b) * (m.n_cu > 0 ? m.n_cu : 1);
+}
+
+// At least this many (tile, group) units per worker: below it, splitting a
+// tile's groups over more workers costs more operand set-up than it gains.
+constexpr int64_t kMinUnitsPerWorker = 8;
+
+template <class Kernel>
+dim3 persistent_grid(Kernel kernel, const DeviceModel& m, int64_t units, int workers_per_block,
+                     int design_per_cu) {
+  const int64_t want = (units + kMinUnitsPerWorker - 1) / kMinUnitsPerWorker;
+  const int64_t blocks_wanted = (want + workers_per_block - 1) / workers_per_block;
+  const int64_t cap = resident_blocks(kernel, m, design_per_cu);
+  return dim3{unsigned(blocks_wanted < cap ? blocks_wanted : cap)};
+}
+
+template <bool kTrans, bool kArticulate>
+hipError_t launch_blend_skin16(const DeviceModel& m, int64_t n, const float* features16,
+                               const float* transforms, const ArticulateArgs& art,
+                               const float* trans, float* verts, float* vposed,
+                               hipStream_t stream) {
+  const int64_t n_quads = ((n + 15) / 16 + 3) / 4;
+  auto kernel = blend_skin16_kernel<kTrans, kArticulate>;
+  const dim3 grid = persistent_grid(kernel, m, n_quads * m.n_groups16, 1, kBlendSkinBlocksPerCU);
+  hipLaunchKernelGGL(kernel, grid, dim3(256), 0, stream, features16, transforms, art, m.basis16,
+                     m.wfrag16, trans, verts, vposed, n, m.n_verts, m.n_groups16);
   return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features16,
+                             const float* transforms, const float* trans, float* verts,
+                             float* vposed, hipStream_t stream) {
+  const ArticulateArgs none{};
+  return trans ? launch_blend_skin16<true, false>(m, n, features16, transforms, none, trans, verts,
+                                                   vposed, stream)
+               : launch_blend_skin16<false, false>(m, n, features16, transforms, none, trans, verts,
+                                                    vposed, stream);
+}
+
+hipError_t launch_forward(const DeviceModel& m, int64_t n, const float* betas,
+                          int64_t betas_stride, const float* pose, const float* trans,
+                          float* verts, float* joints, float* vposed, float* rest_joints,
+                          float* rot_mats, hipStream_t stream) {
+  const ArticulateArgs art{betas, betas_stride, pose, m.joint_template, m.joint_shape, m.parents,
+                           m.depth, m.max_depth, joints, rest_joints, rot_mats};
+  return trans ? launch_blend_skin16<true, true>(m, n, nullptr, nullptr, art, trans, verts, vposed,
+                                                  stream)
+               : launch_blend_skin16<false, true>(m, n, nullptr, nullptr, art, trans, verts, vposed,
+                                                   stream);
 }
 
 hipError_t launch_skin(const DeviceModel& m, int64_t n, const float* transforms,
                        const float* vposed, const float* trans, float* verts,
                        hipStream_t stream) {
-  const int64_t runs = (n + 4 * kSkinHands - 1) / (4 * kSkinHands);
-  const unsigned vgroups = unsigned((m.n_verts + 63) / 64);
-  hipLaunchKernelGGL(skin_kernel, dim3(unsigned(runs), vgroups), dim3(256), 0, stream, m.weights,
-                     transforms, vposed, trans ? trans : m.zeros, trans ? 3 : 0, verts, n,
-                     m.n_verts);
+  const int64_t units = (n + 15) / 16 * m.n_groups16;
+  if (trans) {
+    auto kernel = skin16_kernel<true, kSkinDepth>;
+    hipLaunchKernelGGL(kernel, persistent_grid(kernel, m, units, 4, kSkinBlocksPerCU), dim3(256), 0, stream,
+                       transforms, m.wfrag16, vposed, trans, verts, n, m.n_verts, m.n_groups16);
+  } else {
+    auto kernel = skin16_kernel<false, kSkinDepth>;
+    hipLaunchKernelGGL(kernel, persistent_grid(kernel, m, units, 4, kSkinBlocksPerCU), dim3(256), 0, stream,
+                       transforms, m.wfrag16, vposed, trans, verts, n, m.n_verts, m.n_groups16);
+  }
   return hipGetLastError();
 }
 

@@ -173,13 +173,13 @@ class ManoHip:
         rv = buf("rest_verts", (B, V, 3), rest_verts)
         rj = buf("rest_joints", (B, N_JOINTS, 3), rest_joints)
         rm = buf("rot_mats", (B, N_JOINTS, 3, 3), rot_mats)
-        ws, wsb = self._ws_args(B)
+        # One launch; mano_forward needs no workspace (mano_forward_workspace_bytes == 0).
         _abi.check(_abi.lib().mano_forward(
             self._h, B, _ptr(betas), bstride, _ptr(pose), _ptr(trans), _ptr(v), _ptr(j), _ptr(rv),
-            _ptr(rj), _ptr(rm), ws, wsb, _stream_handle(self.device, stream)))
+            _ptr(rj), _ptr(rm), None, 0, _stream_handle(self.device, stream)))
         return res
 
-    # ---- the three kernels one at a time (per-kernel timing / unit checks) ----
+    # ---- the forward pass as separate kernels (per-kernel timing / intermediates) ----
     def stage_articulate(self, betas, pose, trans=None, joints=None, rest_joints=None,
                          rot_mats=None, stream=None):
         B, betas, bstride, pose, trans = self._inputs(betas, pose, trans)

@@ -272,17 +272,29 @@ def test_errors(engine, dev):
         engine.forward(torch.zeros((3, 9), device=dev), torch.zeros((3, 16, 3), device=dev))
     with pytest.raises(ValueError):
         engine.forward(torch.zeros((3, 10)), torch.zeros((3, 16, 3)))
-    # workspace too small -> MANO_ESMALL through the raw ABI
+    # stage calls: workspace too small -> MANO_ESMALL through the raw ABI
     import ctypes
     lib = _abi.lib()
     b = torch.zeros((64, 10), device=dev)
     p = torch.zeros((64, 16, 3), device=dev)
     v = torch.empty((64, 778, 3), device=dev)
     ws = torch.empty(1024, dtype=torch.uint8, device=dev)
-    rc = lib.mano_forward(engine._h, 64, ctypes.c_void_p(b.data_ptr()), 10, ctypes.c_void_p(p.data_ptr()),
-                          None, ctypes.c_void_p(v.data_ptr()), None, None, None, None,
-                          ctypes.c_void_p(ws.data_ptr()), 1024, None)
+    rc = lib.mano_stage_articulate(engine._h, 64, ctypes.c_void_p(b.data_ptr()), 10,
+                                   ctypes.c_void_p(p.data_ptr()), None, None, None, None,
+                                   ctypes.c_void_p(ws.data_ptr()), 1024, None)
     assert rc == _abi.MANO_ESMALL and "workspace" in _abi.last_error()
+    # mano_forward needs no workspace; bad arguments are still refused
+    assert lib.mano_forward_workspace_bytes(engine._h, 64) == 0
+    rc = lib.mano_forward(engine._h, 64, ctypes.c_void_p(b.data_ptr()), 10, ctypes.c_void_p(p.data_ptr()),
+                          None, ctypes.c_void_p(v.data_ptr()), None, None, None, None, None, 0, None)
+    assert rc == _abi.MANO_OK
+    rc = lib.mano_forward(engine._h, 64, ctypes.c_void_p(b.data_ptr()), 5, ctypes.c_void_p(p.data_ptr()),
+                          None, ctypes.c_void_p(v.data_ptr()), None, None, None, None, None, 0, None)
+    assert rc == _abi.MANO_EINVAL and "betas_stride" in _abi.last_error()
+    rc = lib.mano_forward(engine._h, 64, ctypes.c_void_p(b.data_ptr()), 10, None, None,
+                          ctypes.c_void_p(v.data_ptr()), None, None, None, None, None, 0, None)
+    assert rc == _abi.MANO_EINVAL
+    torch.cuda.synchronize()
 
 
 def test_dropin_quirks(params):
@@ -325,3 +337,32 @@ def test_fused_equals_unfused(engine, dev, params, B):
     assert torch.equal(fused["verts"], v)
     ref = mano_oracle.forward(params, host(betas), host(pose), host(trans))
     assert np.abs(host(v) - ref["verts"]).max() <= TOL_M
+
+
+@pytest.mark.parametrize("B,shared,with_trans", [(1, False, True), (17, True, False),
+                                                 (200, False, False), (4096, False, True)])
+def test_forward_equals_staged(engine, dev, params, B, shared, with_trans):
+    """The single-launch forward (articulation fused into blend_skin16) ==
+    articulate + blend_skin16 staged, bit for bit, for every output."""
+    rng = np.random.default_rng(300 + B)
+    betas = f32(rng.normal(0, 1, (10,) if shared else (B, 10)), dev)
+    pose = f32(rng.normal(0, 0.6, (B, 16, 3)), dev)
+    trans = f32(rng.uniform(-1, 1, (B, 3)), dev) if with_trans else None
+    one = engine.forward(betas, pose, trans, joints=True, rest_verts=True, rest_joints=True,
+                         rot_mats=True)
+    j = torch.empty((B, 16, 3), device=dev)
+    rj = torch.empty((B, 16, 3), device=dev)
+    rm = torch.empty((B, 16, 3, 3), device=dev)
+    v = torch.empty((B, 778, 3), device=dev)
+    vp = torch.empty((B, 778, 3), device=dev)
+    engine.stage_articulate(betas, pose, trans, joints=j, rest_joints=rj, rot_mats=rm)
+    engine.stage_blend_skin(B, v, rest_verts=vp, trans=trans)
+    torch.cuda.synchronize()
+    for name, staged in (("verts", v), ("rest_verts", vp), ("joints", j), ("rest_joints", rj),
+                         ("rot_mats", rm)):
+        assert torch.equal(one[name], staged), name
+    b = host(betas)
+    ref = mano_oracle.forward(params, np.broadcast_to(b, (B, 10)) if shared else b, host(pose),
+                              None if trans is None else host(trans))
+    assert np.abs(host(one["verts"]) - ref["verts"]).max() <= TOL_M
+    assert np.abs(host(one["joints"]) - ref["joints"]).max() <= TOL_M

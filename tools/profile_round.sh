@@ -1,6 +1,8 @@
 #!/bin/bash
 # rocprofv3 evidence for one round: kernel-trace stats of the default bench and
-# separate PMC passes (FETCH_SIZE / WRITE_SIZE / SQ) of the fused and unfused paths.
+# separate PMC passes (FETCH_SIZE / WRITE_SIZE / SQ / L2).  The default bench
+# times the fused forward and, after its timed region, the staged and unfused
+# kernels, so one run covers every kernel.
 # Usage: bash tools/profile_round.sh r01
 set -u
 TAG=${1:-r01}
@@ -16,12 +18,10 @@ run() {  # name timeout args...
   if [ $rc -ne 0 ]; then tail -5 "$OUT/$name.log"; exit $rc; fi
 }
 run stats 300 rocprofv3 --kernel-trace --stats -d $OUT/stats -o bench --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu
-cp $OUT/stats.log $OUT/bench_stats_run.log
-for path in fused unfused; do
-  run fetch_$path 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch_$path -o p --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu --path $path
-  run write_$path 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write_$path -o p --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu --path $path
-  run sq_$path 300 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_COEXEC_CYCLES SQ_WAVE_CYCLES -d $OUT/sq_$path -o p --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu --path $path
-  run l2_$path 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT TCC_HIT_sum TCC_MISS_sum -d $OUT/l2_$path -o p --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu --path $path
-done
+B="python bench.py --steps 5 --warmup 2 --no-cpu"
+run fetch 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o p --output-format csv -- $B
+run write 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o p --output-format csv -- $B
+run sq 300 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES -d $OUT/sq -o p --output-format csv -- $B
+run l2 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT TCC_HIT_sum TCC_MISS_sum -d $OUT/l2 -o p --output-format csv -- $B
 python tools/summarize_pmc.py $OUT > $OUT/summary.txt 2>&1; echo summarize rc=$?
-cat $OUT/summary.txt | head -60
+head -80 $OUT/summary.txt

@@ -13,35 +13,37 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = {"blend_skin_reg_kernel": "blend_skin", "blend_skin_kernel": "blend_skin",
-           "blend_kernel": "blend", "skin_kernel": "skin", "articulate_kernel": "articulate"}
+# demangled-name prefix -> bench.py kernel key (the fused forward is the
+# blend_skin16 instantiation with the articulation prologue, <kTrans, true>)
+KERNELS = {"blend_skin16_kernel<false, true>": "forward", "blend_skin16_kernel<true, true>": "forward",
+           "blend_skin16_kernel<false, false>": "blend_skin",
+           "blend_skin16_kernel<true, false>": "blend_skin",
+           "blend_kernel(": "blend", "skin16_kernel<": "skin", "articulate_kernel(": "articulate"}
 # FETCH_SIZE correction per kernel: x2 where the reads are 16-B-per-lane streams
 # (MI355X_MICROARCH.md §HBM); x1 where the dominant reads are 12-B (dwordx3) or
 # scattered, for which the raw counter already matches the algorithmic bytes
 # (skin: raw FETCH_SIZE 705 MB vs 662 MB algorithmic at 65,536 hands).
-FETCH_FACTOR = {"blend_skin": 2.0, "blend": 2.0, "skin": 1.0, "articulate": 1.0}
+FETCH_FACTOR = {"forward": 2.0, "blend_skin": 2.0, "blend": 2.0, "skin": 1.0, "articulate": 1.0}
 
 
 def short(name):
-    for k, v in KERNELS.items():  # longest names first (dict order above)
-        if "::" + k + "<" in name or "::" + k + "(" in name:
+    for k, v in KERNELS.items():
+        if "::" + k in name:
             return v
     return None
 
 
 def main(d):
-    acc = defaultdict(lambda: defaultdict(list))
+    acc = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> per-dispatch values
     for f in glob.glob(os.path.join(d, "*", "*counter_collection.csv")):
-        path = os.path.basename(os.path.dirname(f)).split("_")[-1]
         for r in csv.DictReader(open(f)):
             k = short(r["Kernel_Name"])
-            if k is None:
-                continue
-            acc[(k, path)][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            if k is not None:
+                acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     out = {"batch": 65536, "kernels": {}}
-    for (k, path), cs in sorted(acc.items()):
+    for k, cs in sorted(acc.items()):
         avg = {c: sum(v) / len(v) for c, v in cs.items()}
-        print(f"{k:12s} [{path}]")
+        print(f"{k:12s}")
         for c, v in sorted(avg.items()):
             print(f"    {c:32s} {v:.6g}")
         if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
@@ -50,7 +52,7 @@ def main(d):
             print(f"    -> hbm read {rd/1e6:.1f} MB ({FETCH_FACTOR[k]:g}x FETCH_SIZE), write {wr/1e6:.1f} MB per launch")
             out["kernels"][k] = {"hbm_bytes_per_launch": rd + wr, "hbm_read_bytes": rd,
                                  "hbm_write_bytes": wr, "fetch_size_kb": avg["FETCH_SIZE"],
-                                 "write_size_kb": avg["WRITE_SIZE"], "path": path,
+                                 "write_size_kb": avg["WRITE_SIZE"],
                                  "fetch_factor": FETCH_FACTOR[k]}
     print(json.dumps(out))
 
