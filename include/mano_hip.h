@@ -83,7 +83,9 @@ size_t mano_workspace_bytes(const mano_model* model, int64_t n_hands);
 size_t mano_forward_workspace_bytes(const mano_model* model, int64_t n_hands);
 
 /* Byte offsets of the intermediates inside the workspace (for inspection):
- * pose-feature operand tiles, skinning transforms [n][16][3][4], v_posed. */
+ * the blend-GEMM A operand rows X [n][160] = [beta | R - I features | 1 | 0..]
+ * stored k-permuted (element k at 16(k>>4) + 4(k&3) + ((k>>2)&3)), the
+ * skinning transforms [n][16][3][4], v_posed [n][V][3]. */
 int mano_workspace_offsets(const mano_model* model, int64_t n_hands,
                            size_t* features_off, size_t* transforms_off,
                            size_t* vposed_off);

@@ -320,8 +320,7 @@ int mano_stage_articulate(const mano_model* m, int64_t n, const float* betas,
   char* base = static_cast<char*>(ws);
   hipError_t e = mano::launch_articulate(
       m->dm, n, betas, betas_stride, pose, trans, reinterpret_cast<float*>(base + w.features_off),
-      reinterpret_cast<float*>(base + w.transforms_off),
-      reinterpret_cast<float*>(base + w.features16_off), joints, rest_joints, rot_mats,
+      reinterpret_cast<float*>(base + w.transforms_off), joints, rest_joints, rot_mats,
       static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "articulate launch");
   return MANO_OK;
@@ -375,7 +374,7 @@ int mano_stage_blend_skin(const mano_model* m, int64_t n, float* rest_verts, con
   const mano::Workspace w = mano::workspace_layout(m->dm, n);
   char* base = static_cast<char*>(ws);
   hipError_t e = mano::launch_blend_skin(
-      m->dm, n, reinterpret_cast<const float*>(base + w.features16_off),
+      m->dm, n, reinterpret_cast<const float*>(base + w.features_off),
       reinterpret_cast<const float*>(base + w.transforms_off), trans, verts, rest_verts,
       static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "blend_skin launch");

@@ -23,10 +23,19 @@ constexpr int kTileFloats = kKGroups * 64 * 4; // 4864 floats = 19,456 B per til
 constexpr int kHandTile = 32;                  // hands per MFMA row tile
 constexpr int kColTile = 32;                   // basis columns per MFMA col tile
 constexpr int kTransformFloats = kJoints * 12; // 3x4 skinning transform per joint
+// Blend GEMM A operand X (the per-hand row [beta | features | 1 | 0 ...]) in
+// the workspace: one row of kXStride floats per hand, k-permuted within each
+// block of 16 so that a v_mfma_f32_16x16x4_f32 A-fragment lane reads its four
+// consecutive steps with one dwordx4: row position 16 g + 4 r + q holds
+//   k = 16 g + 4 q + r        (r = lane >> 4 of the reading lane, q = step % 4)
+// i.e. x_pos(k) = 16 (k >> 4) + 4 (k & 3) + ((k >> 2) & 3).  K is padded to
+// 160 with zeros (X[:, 145] = 1 multiplies the template row of the basis).
+constexpr int kXStride = 160;
+__host__ __device__ constexpr int x_pos(int k) { return 16 * (k >> 4) + 4 * (k & 3) + ((k >> 2) & 3); }
 // Fused blend_skin kernel operands (v_mfma_f32_16x16x4_f32, 16-hand tiles,
 // 16-vertex groups; the LBS transforms T_{c,k}[hand][v] = sum_j A_j[c][k] W[v][j]
 // are one 16x16 tile per (c, k) over K = 16 joints):
-//   features16 per 16 hands: [10][64][4], lane l, step s = 4g + q:
+//   A fragments (from X) per 16 hands, lane l, step s = 4g + q:
 //       X[16 t + (l & 15)][k = 4 s + (l >> 4)]            (K padded to 160)
 //   basis16 per vertex group (3 tiles x, y, z): [10][64][4]:
 //       B[k = 4 s + (l >> 4)][3 (vb + (l & 15)) + coord]
@@ -61,18 +70,16 @@ struct DeviceModel {
 
 // Workspace carving (all offsets 256-B aligned).
 struct Workspace {
-  size_t features_off, transforms_off, features16_off, vposed_off, total;
+  size_t features_off, transforms_off, vposed_off, total;
 };
 
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 inline Workspace workspace_layout(const DeviceModel& m, int64_t n) {
   Workspace w;
-  const int64_t n_tiles = (n + kHandTile - 1) / kHandTile;
   w.features_off = 0;
-  w.transforms_off = align256(w.features_off + size_t(n_tiles) * kTileFloats * sizeof(float));
-  w.features16_off = align256(w.transforms_off + size_t(n) * kTransformFloats * sizeof(float));
-  w.vposed_off = align256(w.features16_off + size_t(2 * n_tiles) * kTile16Floats * sizeof(float));
+  w.transforms_off = align256(w.features_off + size_t(n) * kXStride * sizeof(float));
+  w.vposed_off = align256(w.transforms_off + size_t(n) * kTransformFloats * sizeof(float));
   w.total = align256(w.vposed_off + size_t(n) * m.n_cols * sizeof(float));
   return w;
 }
@@ -80,12 +87,11 @@ inline Workspace workspace_layout(const DeviceModel& m, int64_t n) {
 // Kernel launchers (mano_kernels.hip).  All asynchronous on `stream`.
 hipError_t launch_articulate(const DeviceModel& m, int64_t n, const float* betas,
                              int64_t betas_stride, const float* pose, const float* trans,
-                             float* features, float* transforms, float* features16,
-                             float* joints,
+                             float* features, float* transforms, float* joints,
                              float* rest_joints, float* rot_mats, hipStream_t stream);
 hipError_t launch_blend(const DeviceModel& m, int64_t n, const float* features,
                         float* vposed, hipStream_t stream);
-hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features16,
+hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features,
                              const float* transforms, const float* trans, float* verts,
                              float* vposed, hipStream_t stream);
 // The whole forward pass in one launch (articulation fused into blend_skin16).

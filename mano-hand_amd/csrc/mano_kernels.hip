@@ -48,10 +48,14 @@ __device__ __forceinline__ void rodrigues_minus_eye(float x, float y, float z, f
     a = 1.0f - th2 * (1.0f / 6.0f) + th2 * th2 * (1.0f / 120.0f);
     b = 0.5f - th2 * (1.0f / 24.0f) + th2 * th2 * (1.0f / 720.0f);
   } else {
+    // One sincos of the half angle: sin(theta) = 2 sin(theta/2) cos(theta/2).
     const float th = sqrtf(th2);
-    a = sinf(th) / th;
-    const float sh = sinf(0.5f * th) / th;
-    b = 2.0f * sh * sh;
+    const float inv = 1.0f / th;
+    float sh, ch;
+    sincosf(0.5f * th, &sh, &ch);
+    a = 2.0f * sh * ch * inv;
+    const float shr = sh * inv;
+    b = 2.0f * shr * shr;
   }
   rm[0] = b * (x * x - th2);
   rm[1] = fmaf(b, x * y, -a * z);
@@ -155,83 +159,69 @@ __device__ __forceinline__ void store_joint_outputs(int64_t h, int j, const floa
 
 // Element k of hand row `hl` (0..15) of the blend GEMM A operand X in the
 // 16x16x4 fragment layout: step s = k / 4, lane hl + 16 (k & 3), packed as
-// [s / 4][64 lanes][s % 4] (mano_internal.h).
+// [s / 4][64 lanes][s % 4] (the fused forward's LDS staging).
 __device__ __forceinline__ int x16_index(int hl, int k) {
   const int s = k >> 2;
   return (((s >> 2) * 64) + hl + 16 * (k & 3)) * 4 + (s & 3);
 }
 
 // ---------------------------------------------------------------------------
-// articulate: 512 threads = 32 hands x 16 joints = exactly one MFMA hand tile.
+// articulate: one lane per (hand, joint), 16 hands per 256-thread block.  The
+// X rows (kXStride floats, k-permuted, mano_internal.h) are assembled in LDS
+// -- each lane drops its 9 features in place -- and leave as one contiguous
+// 10-KB dwordx4 stream; transforms and joints are stored straight from the
+// lanes (48 and 12 contiguous bytes each).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(512) void articulate_kernel(
+__global__ __launch_bounds__(256) void articulate_kernel(
     const float* __restrict__ betas, int64_t betas_stride, const float* __restrict__ pose,
     const float* __restrict__ trans, const float* __restrict__ joint_template,
     const float* __restrict__ joint_shape, const int32_t* __restrict__ parents,
     const int32_t* __restrict__ depth, int max_depth, int64_t n,
-    float* __restrict__ features, float* __restrict__ transforms,
-    float* __restrict__ features16, float* __restrict__ joints,
+    float* __restrict__ features, float* __restrict__ transforms, float* __restrict__ joints,
     float* __restrict__ rest_joints, float* __restrict__ rot_mats) {
-  __shared__ f32x4 tile[kKGroups * 64];
-  __shared__ f32x4 tile16[2 * kTile16Floats / 4];
-  float* tilef = reinterpret_cast<float*>(tile);
-  float* tile16f = reinterpret_cast<float*>(tile16);
-
+  __shared__ f32x4 xs4[16 * kXStride / 4];
+  float* xs = reinterpret_cast<float*>(xs4);
   const int tid = threadIdx.x;
   const int j = tid & (kJoints - 1);
-  const int hl = tid >> 4;  // hand within the tile
-  const int64_t h = int64_t(blockIdx.x) * kHandTile + hl;
-  const bool valid = h < n;
+  const int hl = tid >> 4;
+  const int64_t h0 = int64_t(blockIdx.x) * 16;
+  const int64_t h = min(h0 + hl, n - 1);  // tail lanes repeat the last hand
+  const bool valid = h0 + hl < n;
 
-  float x = 0.f, y = 0.f, z = 0.f;
-  if (valid) {
-    const float* p = pose + h * (kJoints * 3) + 3 * j;
-    x = p[0];
-    y = p[1];
-    z = p[2];
-  }
+  const float* p = pose + h * (kJoints * 3) + 3 * j;
   float beta[kShape];
 #pragma unroll
-  for (int s = 0; s < kShape; ++s) beta[s] = valid ? betas[h * betas_stride + s] : 0.f;
+  for (int s = 0; s < kShape; ++s) beta[s] = betas[h * betas_stride + s];
   const int par = parents[j];
   const int src = ((tid & 63) & ~(kJoints - 1)) + (par < 0 ? 0 : par);
   float rm[9], J[3], t[3], Aj[12];
-  articulate_joint(x, y, z, beta, j, src, depth[j], max_depth, joint_template, joint_shape, rm, J,
-                   t, Aj);
+  articulate_joint(p[0], p[1], p[2], beta, j, src, depth[j], max_depth, joint_template, joint_shape,
+                   rm, J, t, Aj);
   if (valid) {
-    float* A = transforms + h * kTransformFloats + j * 12;
-#pragma unroll
-    for (int m = 0; m < 12; ++m) A[m] = Aj[m];
+    f32x4* A = reinterpret_cast<f32x4*>(transforms + h * kTransformFloats + j * 12);
+    A[0] = f32x4{Aj[0], Aj[1], Aj[2], Aj[3]};
+    A[1] = f32x4{Aj[4], Aj[5], Aj[6], Aj[7]};
+    A[2] = f32x4{Aj[8], Aj[9], Aj[10], Aj[11]};
     store_joint_outputs(h, j, trans, rm, J, t, joints, rest_joints, rot_mats);
   }
 
-  // Blend-GEMM A operand: X[h][k], k < 10 beta, 10 <= k < 145 features
-  // (k = 10 + 9(j-1) + 3 row + col, the ravel order of :91), X[h][145] = 1
-  // (selects the template row of the basis), zeros up to the padded K.
-  // 32x32x2 layout (blend kernel): step s = k/2 holds X[hand = lane & 31][k =
-  // 2s + (lane >> 5)], 4 steps per float4; 16x16x4 layout: x16_index.
-  float* t16 = tile16f + (hl >> 4) * kTile16Floats;
-  auto put = [&](int k, float v) {
-    const int s = k >> 1;
-    const int ln = hl + 32 * (k & 1);
-    if (k < kKGroups * 8) tilef[(((s >> 2) * 64) + ln) * 4 + (s & 3)] = v;
-    if (k < kGroups16 * 16) t16[x16_index(hl & 15, k)] = v;
-  };
+  // Row of X: k < 10 beta, 10 <= k < 145 features (k = 10 + 9(j-1) + 3 row +
+  // col, the ravel order of :91), X[h][145] = 1, zeros up to kXStride.
+  float* x = xs + hl * kXStride;
   if (j == 0) {
 #pragma unroll
-    for (int s = 0; s < kShape; ++s) put(s, beta[s]);
-    put(kK, 1.f);  // X[:, 145] = 1 multiplies the template row of the basis
+    for (int s = 0; s < kShape; ++s) x[x_pos(s)] = beta[s];
+    x[x_pos(kK)] = 1.f;
 #pragma unroll
-    for (int k = kK + 1; k < kGroups16 * 16; ++k) put(k, 0.f);
+    for (int k = kK + 1; k < kXStride; ++k) x[x_pos(k)] = 0.f;
   } else {
 #pragma unroll
-    for (int m = 0; m < 9; ++m) put(kShape + 9 * (j - 1) + m, rm[m]);
+    for (int m = 0; m < 9; ++m) x[x_pos(kShape + 9 * (j - 1) + m)] = rm[m];
   }
   __syncthreads();
-  f32x4* dst = reinterpret_cast<f32x4*>(features + int64_t(blockIdx.x) * kTileFloats);
-  for (int i = tid; i < kKGroups * 64; i += 512) dst[i] = tile[i];
-  f32x4* d16 = reinterpret_cast<f32x4*>(features16 + int64_t(blockIdx.x) * 2 * kTile16Floats);
-  for (int i = tid; i < 2 * kTile16Floats / 4; i += 512) d16[i] = tile16[i];
+  const int n_rows = int(n - h0 < 16 ? n - h0 : 16);
+  f32x4* dst = reinterpret_cast<f32x4*>(features + h0 * kXStride);
+  for (int i = tid; i < n_rows * (kXStride / 4); i += 256) dst[i] = xs4[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -301,17 +291,14 @@ __global__ __launch_bounds__(256, 2) void blend_kernel(
   const int64_t n_ht = (n + kHandTile - 1) / kHandTile;
   const bool active = ht < n_ht;
 
+  // A fragments of v_mfma_f32_32x32x2_f32: step s holds X[hand = lane & 31][k =
+  // 2 s + (lane >> 5)] (X rows past the batch end repeat the last hand).
   float a[kKGroups * 4];
   {
-    const f32x4* src = reinterpret_cast<const f32x4*>(features + (active ? ht : 0) * kTileFloats) + lane;
+    const int64_t row = min((active ? ht : 0) * kHandTile + (lane & 31), n - 1);
+    const float* x = features + row * kXStride;
 #pragma unroll
-    for (int g = 0; g < kKGroups; ++g) {
-      const f32x4 v = src[g * 64];
-      a[4 * g + 0] = v[0];
-      a[4 * g + 1] = v[1];
-      a[4 * g + 2] = v[2];
-      a[4 * g + 3] = v[3];
-    }
+    for (int s = 0; s < kKGroups * 4; ++s) a[s] = s < kKSteps ? x[x_pos(2 * s + (lane >> 5))] : 0.f;
   }
 
   stage_basis_tile(basis_tiles, 0, bs[0], wave, lane);
@@ -484,7 +471,7 @@ __device__ __forceinline__ void unit_range(int64_t units, int64_t worker, int64_
 // in LDS by LDS-DMA one tile ahead, then the LBS epilogue.
 template <bool kTrans, bool kArticulate>
 __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
-    const float* __restrict__ features16, const float* __restrict__ transforms,
+    const float* __restrict__ features, const float* __restrict__ transforms,
     ArticulateArgs art, const float* __restrict__ basis16, const float* __restrict__ wfrag16,
     const float* __restrict__ trans, float* __restrict__ verts, float* __restrict__ vposed,
     int64_t n, int n_verts, int n_groups) {
@@ -593,10 +580,12 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
       }
       __syncthreads();  // the basis ring overwrites the staging areas next
     } else {
-      const f32x4* src = reinterpret_cast<const f32x4*>(features16 + tc * kTile16Floats) + lane;
+      // A fragments from the X rows: lane's steps 4g..4g+3 are one dwordx4.
+      const int64_t row = min(h0 + (lane & 15), n - 1);
+      const f32x4* src = reinterpret_cast<const f32x4*>(features + row * kXStride) + (lane >> 4);
 #pragma unroll
       for (int g = 0; g < kGroups16; ++g) {
-        const f32x4 v = src[g * 64];
+        const f32x4 v = src[4 * g];
 #pragma unroll
         for (int q = 0; q < 4; ++q) a[4 * g + q] = v[q];
       }
@@ -791,14 +780,12 @@ __global__ __launch_bounds__(256) void rodrigues_kernel(const float* __restrict_
 
 hipError_t launch_articulate(const DeviceModel& m, int64_t n, const float* betas,
                              int64_t betas_stride, const float* pose, const float* trans,
-                             float* features, float* transforms, float* features16,
-                             float* joints,
+                             float* features, float* transforms, float* joints,
                              float* rest_joints, float* rot_mats, hipStream_t stream) {
-  const int64_t blocks = (n + kHandTile - 1) / kHandTile;
-  hipLaunchKernelGGL(articulate_kernel, dim3(unsigned(blocks)), dim3(512), 0, stream, betas,
+  const int64_t blocks = (n + 15) / 16;
+  hipLaunchKernelGGL(articulate_kernel, dim3(unsigned(blocks)), dim3(256), 0, stream, betas,
                      betas_stride, pose, trans, m.joint_template, m.joint_shape, m.parents,
-                     m.depth, m.max_depth, n, features, transforms, features16, joints,
-                     rest_joints, rot_mats);
+                     m.depth, m.max_depth, n, features, transforms, joints, rest_joints, rot_mats);
   return hipGetLastError();
 }
 
@@ -844,27 +831,27 @@ dim3 persistent_grid(Kernel kernel, const DeviceModel& m, int64_t units, int wor
 }
 
 template <bool kTrans, bool kArticulate>
-hipError_t launch_blend_skin16(const DeviceModel& m, int64_t n, const float* features16,
+hipError_t launch_blend_skin16(const DeviceModel& m, int64_t n, const float* features,
                                const float* transforms, const ArticulateArgs& art,
                                const float* trans, float* verts, float* vposed,
                                hipStream_t stream) {
   const int64_t n_quads = ((n + 15) / 16 + 3) / 4;
   auto kernel = blend_skin16_kernel<kTrans, kArticulate>;
   const dim3 grid = persistent_grid(kernel, m, n_quads * m.n_groups16, 1, kBlendSkinBlocksPerCU);
-  hipLaunchKernelGGL(kernel, grid, dim3(256), 0, stream, features16, transforms, art, m.basis16,
+  hipLaunchKernelGGL(kernel, grid, dim3(256), 0, stream, features, transforms, art, m.basis16,
                      m.wfrag16, trans, verts, vposed, n, m.n_verts, m.n_groups16);
   return hipGetLastError();
 }
 
 }  // namespace
 
-hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features16,
+hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features,
                              const float* transforms, const float* trans, float* verts,
                              float* vposed, hipStream_t stream) {
   const ArticulateArgs none{};
-  return trans ? launch_blend_skin16<true, false>(m, n, features16, transforms, none, trans, verts,
+  return trans ? launch_blend_skin16<true, false>(m, n, features, transforms, none, trans, verts,
                                                    vposed, stream)
-               : launch_blend_skin16<false, false>(m, n, features16, transforms, none, trans, verts,
+               : launch_blend_skin16<false, false>(m, n, features, transforms, none, trans, verts,
                                                     vposed, stream);
 }
 

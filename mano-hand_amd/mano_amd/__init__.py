@@ -8,8 +8,8 @@ Drop-in for reyuwei/MANO-Hand's `mano_np.MANOModel`:
 
 Batched device API: `ManoHip(params).forward(betas, pose, trans)`.
 """
-from .model_io import (MANO_PARENTS, MODEL_KEYS, load_dump, params_digest, save_dump,  # noqa: F401
-                       synthetic_params)
+from .model_io import (MANO_PARENTS, MODEL_KEYS, dump_model, load_dump, load_official,  # noqa: F401
+                       params_digest, save_dump, synthetic_params)
 
 
 def __getattr__(name):
@@ -21,4 +21,5 @@ def __getattr__(name):
 
 
 __all__ = ["MANOModel", "ManoHip", "write_obj", "load_dump", "save_dump", "synthetic_params",
+           "load_official", "dump_model",
            "params_digest", "MANO_PARENTS", "MODEL_KEYS"]

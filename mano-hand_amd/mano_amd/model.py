@@ -39,6 +39,13 @@ def _stream_handle(device: torch.device, stream=None):
     return ctypes.c_void_p(s.cuda_stream)
 
 
+# Workspace row layout of the blend-GEMM A operand (mano_internal.h x_pos):
+# element k of a hand's X row sits at X_POS[k], so that a 16x16x4 MFMA
+# fragment lane reads its four consecutive K steps with one 16-byte load.
+X_STRIDE = 160
+X_POS = np.array([16 * (k >> 4) + 4 * (k & 3) + ((k >> 2) & 3) for k in range(X_STRIDE)])
+
+
 class ManoHip:
     """Device-resident MANO model on one GPU (wraps a `mano_model*` handle)."""
 
@@ -208,17 +215,18 @@ class ManoHip:
                                                     _stream_handle(self.device, stream)))
 
     def intermediates(self, n: int) -> Dict[str, torch.Tensor]:
-        """Views of the workspace after a stage/forward call over `n` hands:
-        `features` (ceil(n/32), 19, 64, 4) MFMA A tiles, `transforms`
-        (n,16,3,4) skinning transforms, `vposed` (n,V,3)."""
+        """Views of the workspace after the stage calls over `n` hands:
+        `features` (n, 160) the blend-GEMM A operand rows X = [beta | R-I
+        features | 1 | 0...] in the kernels' k-permuted order (`X[:, k] =
+        features[:, X_POS[k]]`), `transforms` (n,16,3,4) skinning transforms,
+        `vposed` (n,V,3)."""
         ws = self.workspace(n)
         base = ws.data_ptr()
         shift = ((base + 255) & ~255) - base
         fo, to, vo = self.workspace_offsets(n)
         f32 = ws[shift:shift + (ws.numel() - shift) // 4 * 4].view(torch.float32)
-        nt = (n + 31) // 32
         return {
-            "features": f32[fo // 4: fo // 4 + nt * 4864].view(nt, 19, 64, 4),
+            "features": f32[fo // 4: fo // 4 + n * X_STRIDE].view(n, X_STRIDE),
             "transforms": f32[to // 4: to // 4 + n * 192].view(n, N_JOINTS, 3, 4),
             "vposed": f32[vo // 4: vo // 4 + n * self.n_verts * 3].view(n, self.n_verts, 3),
         }

@@ -113,6 +113,128 @@ def save_dump(params: Dict[str, object], path: str) -> None:
         pickle.dump(out, f)
 
 
+# ---------------------------------------------------------------------------
+# Official MANO_{LEFT,RIGHT}.pkl ingestion without chumpy.
+#
+# The official pickle (Python 2, read by the reference with
+# `pickle.load(f, encoding='latin1')`, dump_model.py:6) stores chumpy `Ch`
+# objects for weights / posedirs / shapedirs / v_template, a scipy CSC matrix
+# for J_regressor and numpy arrays for the rest.  dump_model.py needs chumpy
+# and scipy installed to rebuild them and then converts each to an array
+# (dump_model.py:8-18).  `load_official` rebuilds the same arrays with a
+# restricted unpickler that executes nothing: chumpy / scipy globals resolve to
+# inert record classes that only keep their pickled state, and the arrays are
+# read out of that state (a leaf `Ch` keeps its value in `x`; a CSC matrix in
+# `data` / `indices` / `indptr` / `_shape`).  Parity unpinned: no official
+# pickle exists here; tests/test_model_io.py checks the loader on pickles made
+# with stand-in classes of the same module/class names and state fields.
+# ---------------------------------------------------------------------------
+class _Record:
+    """Inert stand-in for a chumpy / scipy object: keeps the pickled state."""
+
+    _origin = ""
+
+    def __init__(self, *args, **kwargs):
+        self.__dict__["_args"] = args
+
+    def __setstate__(self, state):
+        if isinstance(state, tuple) and len(state) == 2:  # (dict, slots) form
+            state = {**(state[0] or {}), **(state[1] or {})}
+        if isinstance(state, dict):
+            self.__dict__.update({_norm_key(k): v for k, v in state.items()})
+
+
+class _ChRecord(_Record):
+    _origin = "chumpy"
+
+
+class _CscRecord(_Record):
+    _origin = "scipy.sparse csc_matrix"
+
+
+def _safe_reconstructor(cls, base, state):
+    """copyreg._reconstructor restricted to the record classes (protocol 0/1 pickles)."""
+    if not (isinstance(cls, type) and issubclass(cls, _Record)) or base is not object:
+        raise pickle.UnpicklingError(f"refusing to reconstruct {cls!r} from a model file")
+    obj = cls.__new__(cls)
+    obj.__dict__["_args"] = ()
+    return obj
+
+
+# builtins a chumpy object's state may hold (its caches and flags); constructing
+# them from pickled data runs no user code.
+_INERT_BUILTINS = {"object": object, "set": set, "frozenset": frozenset, "list": list,
+                   "dict": dict, "tuple": tuple}
+
+
+class _OfficialUnpickler(_ArrayOnlyUnpickler):
+    """numpy arrays + inert records of chumpy / scipy.sparse objects, nothing else."""
+
+    def find_class(self, module, name):
+        if module.startswith("chumpy"):
+            return _ChRecord
+        if module.startswith("scipy.sparse") and name == "csc_matrix":
+            return _CscRecord
+        if (module, name) in (("copy_reg", "_reconstructor"), ("copyreg", "_reconstructor")):
+            return _safe_reconstructor
+        if module in ("__builtin__", "builtins") and name in _INERT_BUILTINS:
+            return _INERT_BUILTINS[name]
+        return super().find_class(module, name)
+
+
+def _as_array(v, key):
+    if isinstance(v, _ChRecord):
+        if "x" not in v.__dict__:
+            raise ValueError(f"{key}: chumpy object without a stored value 'x' "
+                             "(a derived expression); cannot convert without chumpy")
+        return np.asarray(v.__dict__["x"])
+    if isinstance(v, _CscRecord):
+        return _csc_dense(v, key)
+    return np.asarray(v)
+
+
+def _csc_dense(v, key):
+    d = v.__dict__
+    try:
+        data, indices, indptr = (np.asarray(d[k]) for k in ("data", "indices", "indptr"))
+        shape = tuple(int(x) for x in d.get("_shape", d.get("shape")))
+    except (KeyError, TypeError) as e:
+        raise ValueError(f"{key}: unrecognised CSC matrix state {sorted(d)}") from e
+    out = np.zeros(shape, dtype=data.dtype)
+    for c in range(shape[1]):  # column c holds rows indices[indptr[c]:indptr[c+1]]
+        lo, hi = int(indptr[c]), int(indptr[c + 1])
+        out[indices[lo:hi], c] += data[lo:hi]
+    return out
+
+
+def load_official(path: str) -> Dict[str, object]:
+    """Official MANO pickle -> the nine-key dump layout (dump_model.py:4-18), no chumpy."""
+    with open(path, "rb") as f:
+        data = _OfficialUnpickler(f, encoding="latin1").load()
+    if not isinstance(data, dict):
+        raise pickle.UnpicklingError("official model file does not hold a dict")
+    data = {_norm_key(k): v for k, v in data.items()}
+    out = {
+        "pose_pca_basis": _as_array(data["hands_components"], "hands_components"),  # :8
+        "pose_pca_mean": _as_array(data["hands_mean"], "hands_mean"),               # :9
+        "J_regressor": _as_array(data["J_regressor"], "J_regressor"),               # :10
+        "skinning_weights": _as_array(data["weights"], "weights"),                   # :11
+        "mesh_pose_basis": _as_array(data["posedirs"], "posedirs"),                  # :13
+        "mesh_shape_basis": _as_array(data["shapedirs"], "shapedirs"),               # :14
+        "mesh_template": _as_array(data["v_template"], "v_template"),                # :15
+        "faces": _as_array(data["f"], "f"),                                          # :16
+    }
+    parents = _as_array(data["kintree_table"], "kintree_table")[0].tolist()         # :17
+    parents[0] = None                                                                # :18
+    out["parents"] = parents
+    return out
+
+
+def dump_model(src_path: str, dst_path: str) -> None:
+    """dump_model.py:4-21 without chumpy: official pickle -> dump-layout pickle."""
+    save_dump(load_official(src_path), dst_path)
+
+
 def parents_to_int(parents) -> np.ndarray:
     """`parents` list with None at the root -> int32 array with -1 at the root."""
     return np.array([-1 if p is None else int(p) for p in parents], dtype=np.int32)

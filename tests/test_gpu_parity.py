@@ -178,19 +178,14 @@ def test_stage_intermediates(engine, dev, params):
     torch.cuda.synchronize()
     inter = engine.intermediates(B)
     ref = mano_oracle.forward(params, betas, pose)
-    # features: decode the MFMA A tiles back to X[h][k]
-    tiles = host(inter["features"])  # (nt, 19, 64, 4)
-    X = np.zeros((tiles.shape[0] * 32, 152))
-    for g in range(19):
-        for q in range(4):
-            s = 4 * g + q
-            X[:, 2 * s] = tiles[:, g, :32, q].reshape(-1)
-            X[:, 2 * s + 1] = tiles[:, g, 32:, q].reshape(-1)
-    X = X[:B]
+    # features: the X rows, k-permuted in the workspace (model.X_POS)
+    from mano_amd.model import X_POS
+    X = host(inter["features"])[:, X_POS]
     assert np.abs(X[:, :10] - betas).max() < 1e-6
     feats = mano_oracle.pose_features(ref["rot"])
     assert np.abs(X[:, 10:145] - feats).max() <= TOL_R
     assert np.all(X[:, 145] == 1.0) and np.all(X[:, 146:] == 0.0)
+    assert sorted(X_POS.tolist()) == list(range(160))
     # transforms: oracle G after rest removal, rows 0..2
     _, G = mano_oracle.chain(ref["rot"], ref["rest_joints"], params["parents"])
     assert np.abs(host(inter["transforms"]) - G[:, :, :3, :]).max() <= TOL_M

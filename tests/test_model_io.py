@@ -85,3 +85,87 @@ def test_synthetic_model_properties(params):
     assert np.allclose(params["J_regressor"].sum(1), 1.0) and (params["J_regressor"] >= 0).all()
     assert np.allclose(params["skinning_weights"].sum(1), 1.0)
     assert model_io.params_digest(model_io.synthetic_params(0)) == model_io.params_digest(params)
+
+
+# ---- official-pickle ingestion without chumpy ----------
+# chumpy is not installed and no official MANO pickle exists here, so the
+# official file is imitated: a stand-in `chumpy.ch.Ch` class (same module and
+# class name, value kept in `x` as chumpy leaves do) and a real scipy CSC
+# matrix.  Parity with a real MANO_*.pkl is unpinned.
+import sys
+import types
+
+
+def _official_like(params, protocol):
+    scipy_sparse = pytest.importorskip("scipy.sparse")
+    mods = {}
+    for name in ("chumpy", "chumpy.ch"):
+        mods[name] = sys.modules.get(name)
+    pkg = types.ModuleType("chumpy")
+    ch = types.ModuleType("chumpy.ch")
+
+    class Ch(object):
+        def __init__(self, x):
+            self.x = np.asarray(x)
+            self._dirty_vars = set()
+            self.label = None
+
+    Ch.__module__, Ch.__qualname__ = "chumpy.ch", "Ch"
+    ch.Ch = Ch
+    pkg.ch = ch
+    sys.modules["chumpy"], sys.modules["chumpy.ch"] = pkg, ch
+    try:
+        kintree = np.array([[4294967295] + [p for p in params["parents"][1:]], list(range(16))],
+                           dtype=np.int64)
+        official = {
+            "hands_components": np.asarray(params["pose_pca_basis"]),
+            "hands_mean": np.asarray(params["pose_pca_mean"]),
+            "J_regressor": scipy_sparse.csc_matrix(np.asarray(params["J_regressor"])),
+            "weights": Ch(params["skinning_weights"]),
+            "posedirs": Ch(params["mesh_pose_basis"]),
+            "shapedirs": Ch(params["mesh_shape_basis"]),
+            "v_template": Ch(params["mesh_template"]),
+            "f": np.asarray(params["faces"], dtype=np.uint32),
+            "kintree_table": kintree,
+            "J": np.zeros((16, 3)),
+            "bs_style": "lbs",
+            "bs_type": "lrotmin",
+        }
+        return pickle.dumps(official, protocol=protocol)
+    finally:
+        for name, m in mods.items():
+            if m is None:
+                sys.modules.pop(name, None)
+            else:
+                sys.modules[name] = m
+
+
+@pytest.mark.parametrize("protocol", [0, 2])
+def test_load_official_without_chumpy(params, tmp_path, protocol):
+    src = tmp_path / "MANO_LEFT.pkl"
+    src.write_bytes(_official_like(params, protocol))
+    assert "chumpy" not in sys.modules
+    got = model_io.load_official(str(src))
+    assert got["parents"] == model_io.MANO_PARENTS
+    for k in model_io.MODEL_KEYS:
+        if k == "parents":
+            continue
+        a, b = np.asarray(got[k]), np.asarray(params[k])
+        assert a.shape == b.shape and np.array_equal(a, b.astype(a.dtype)), k
+    # dump_model(): official -> dump layout file, readable by load_dump
+    dst = tmp_path / "dump.pkl"
+    model_io.dump_model(str(src), str(dst))
+    back = model_io.load_dump(str(dst))
+    model_io.check_layout(back)
+    assert np.array_equal(np.asarray(back["J_regressor"]), np.asarray(params["J_regressor"]))
+
+
+def test_load_official_refuses_code(tmp_path):
+    class Evil:
+        def __reduce__(self):
+            return (os.system, ("echo pwned",))
+
+    p = tmp_path / "evil.pkl"
+    p.write_bytes(pickle.dumps({"hands_components": Evil()}, protocol=2))
+    with pytest.raises(pickle.UnpicklingError):
+        model_io.load_official(str(p))
