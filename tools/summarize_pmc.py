@@ -19,11 +19,11 @@ KERNELS = {"blend_skin16_kernel<false, true>": "forward", "blend_skin16_kernel<t
            "blend_skin16_kernel<false, false>": "blend_skin",
            "blend_skin16_kernel<true, false>": "blend_skin",
            "blend_kernel(": "blend", "skin16_kernel<": "skin", "articulate_kernel(": "articulate"}
-# FETCH_SIZE correction per kernel: x2 where the reads are 16-B-per-lane streams
-# (MI355X_MICROARCH.md §HBM); x1 where the dominant reads are 12-B (dwordx3) or
-# scattered, for which the raw counter already matches the algorithmic bytes
-# (skin: raw FETCH_SIZE 705 MB vs 662 MB algorithmic at 65,536 hands).
-FETCH_FACTOR = {"forward": 2.0, "blend_skin": 2.0, "blend": 2.0, "skin": 1.0, "articulate": 1.0}
+# FETCH_SIZE correction (MI355X_MICROARCH.md §HBM): on gfx950 the counter
+# reports half the bytes of wide coalesced streams.  Measured here it is x2 for
+# every kernel of this path, dwordx3 streams included: skin16 raw 350.6 MB vs
+# 662 MB algorithmic reads, articulate raw 7.7 MB vs 15.2 MB (65,536 hands).
+FETCH_FACTOR = {"forward": 2.0, "blend_skin": 2.0, "blend": 2.0, "skin": 2.0, "articulate": 2.0}
 
 
 def short(name):
