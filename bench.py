@@ -2,8 +2,8 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--gather]
 
-One step = one forward pass (articulate -> blend GEMM -> LBS; by default the
-single fused launch mano_forward) over B hands per GPU
+One step = one forward pass (mano_forward: articulate, then the fused blend
+GEMM + LBS kernel) over B hands per GPU
 (BASELINE.json configs[1]: 65,536 hands, fp32 full pose, random betas), inputs
 resident in HBM before the timed region.  N > 1 runs one process per GPU
 (torch.distributed.run); shards are independent (no collective on the hot
@@ -43,13 +43,13 @@ PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=65536, help="hands per GPU per step")
     ap.add_argument("--gather", action="store_true", help="RCCL gather of verts+joints to GPU 0")
-    ap.add_argument("--path", choices=("fused", "staged", "unfused"), default="fused",
-                    help="fused: one launch (default); staged: articulate + blend_skin; "
-                         "unfused: articulate + blend + skin")
+    ap.add_argument("--path", choices=("forward", "api", "unfused"), default="forward",
+                    help="forward: mano_forward's two kernels, each bracketed by events (default); "
+                         "api: one mano_forward call per step; unfused: articulate + blend + skin")
     ap.add_argument("--model", default=None, help="dump_model.py pickle (default: synthetic seed 0)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
@@ -121,24 +121,26 @@ def main():
     joints = torch.empty((B, 16, 3), device=dev)
     stream = torch.cuda.current_stream(dev)
     out = {"verts": verts, "joints": joints}
-    if args.path != "fused":
-        model.workspace(B)
+    model.workspace(B)  # allocated before timing (covers every path)
 
     # Launch sequence of one step; `marks` get an event after each kernel.
+    # "forward" issues exactly mano_forward's two launches (articulate, then
+    # the fused blend GEMM + LBS) through the stage calls so that each kernel
+    # is bracketed by events on its stream; "api" is one mano_forward call.
     def run_path(path, marks=None):
         def mark(i):
             if marks is not None:
                 marks[i].record(stream)
         mark(0)
-        if path == "fused":  # one launch: articulate + blend GEMM + LBS
-            model.forward(betas, pose, joints=True, out=out)
-            mark(1)
-        elif path == "staged":  # articulate, then blend GEMM + LBS
+        if path == "forward":
             model.stage_articulate(betas, pose, joints=joints)
             mark(1)
             model.stage_blend_skin(B, verts)
             mark(2)
-        else:  # articulate, blend GEMM (v_posed to HBM), LBS
+        elif path == "api":
+            model.forward(betas, pose, joints=True, out=out)
+            mark(1)
+        else:  # unfused: articulate, blend GEMM (v_posed to HBM), LBS
             model.stage_articulate(betas, pose, joints=joints)
             mark(1)
             model.stage_blend(B)
@@ -146,7 +148,7 @@ def main():
             model.stage_skin(B, verts)
             mark(3)
 
-    n_marks = {"fused": 2, "staged": 3, "unfused": 4}
+    n_marks = {"forward": 3, "api": 2, "unfused": 4}
 
     def step(marks=None):
         run_path(args.path, marks)
@@ -182,20 +184,18 @@ def main():
         return float(np.mean([e[a].elapsed_time(e[b]) for e in evs]))
 
     # Per-kernel table.  The timed path's kernels come from the timed steps;
-    # the other paths' kernels are timed on the same stream afterwards (not
-    # part of `value`), so every kernel's roofline is reported each run.
-    timed = {"fused": {"forward": (0, 1)},
-             "staged": {"articulate": (0, 1), "blend_skin": (1, 2)},
+    # the other paths' kernels are timed on the same stream afterwards (rank 0,
+    # not part of `value`), so every kernel's roofline is reported each run.
+    timed = {"forward": {"articulate": (0, 1), "blend_skin": (1, 2)},
+             "api": {"mano_forward": (0, 1)},
              "unfused": {"articulate": (0, 1), "blend": (1, 2), "skin": (2, 3)}}
     ms = {k: span(a, b, events) for k, (a, b) in timed[args.path].items()}
     if rank == 0:
-        if args.path != "fused":
-            model.workspace(B)
-        for path in ("fused", "staged", "unfused"):
+        for path in ("forward", "api", "unfused"):
             if path == args.path:
                 continue
             evs = [[torch.cuda.Event(enable_timing=True) for _ in range(n_marks[path])]
-                   for _ in range(5)]
+                   for _ in range(20)]
             run_path(path)
             for e in evs:
                 run_path(path, e)
@@ -209,39 +209,42 @@ def main():
     def gbs(nbytes, t):
         return nbytes * B / (t * 1e-3) / 1e9
 
+    in_path = {"forward": ("articulate", "blend_skin"), "api": ("mano_forward",),
+               "unfused": ("articulate", "blend", "skin")}[args.path]
     kernels = {}
-    if "forward" in ms:
-        a = tflops(FUSED_MFMA_FLOP_PER_HAND, ms["forward"])
-        kernels["forward"] = {"kernel": "blend_skin16_kernel<*, true>", "ms": ms["forward"],
-                              "bound": "mfma", "achieved_TFLOPs": a, "frac": a / PEAK_FP32_TFLOPS,
-                              "flop_per_hand": FUSED_MFMA_FLOP_PER_HAND,
-                              "in_timed_path": args.path == "fused"}
+    if "mano_forward" in ms:
+        kernels["mano_forward"] = {"kernel": "articulate_kernel + blend_skin16_kernel (one ABI call)",
+                                   "ms": ms["mano_forward"]}
     if "articulate" in ms:
         a = gbs(ARTICULATE_BYTES_PER_HAND, ms["articulate"])
         kernels["articulate"] = {"kernel": "articulate_kernel", "ms": ms["articulate"],
                                  "bound": "latency", "achieved_GBs": a,
-                                 "in_timed_path": args.path != "fused"}
+                                 "bytes_per_hand": ARTICULATE_BYTES_PER_HAND}
     if "blend_skin" in ms:
         a = tflops(FUSED_MFMA_FLOP_PER_HAND, ms["blend_skin"])
-        kernels["blend_skin"] = {"kernel": "blend_skin16_kernel<*, false>", "ms": ms["blend_skin"],
+        kernels["blend_skin"] = {"kernel": "blend_skin16_kernel", "ms": ms["blend_skin"],
                                  "bound": "mfma", "achieved_TFLOPs": a,
                                  "frac": a / PEAK_FP32_TFLOPS,
-                                 "in_timed_path": args.path == "staged"}
+                                 "flop_per_hand": FUSED_MFMA_FLOP_PER_HAND,
+                                 "blend_gemm_TFLOPs": tflops(BLEND_FLOP_PER_HAND, ms["blend_skin"])}
     if "blend" in ms:
         a = tflops(BLEND_FLOP_PER_HAND, ms["blend"])
         kernels["blend"] = {"kernel": "blend_kernel", "ms": ms["blend"], "bound": "mfma",
                             "achieved_TFLOPs": a, "frac": a / PEAK_FP32_TFLOPS,
-                            "in_timed_path": args.path == "unfused"}
+                            "flop_per_hand": BLEND_FLOP_PER_HAND}
     if "skin" in ms:
         a = gbs(SKIN_BYTES_PER_HAND, ms["skin"])
         kernels["skin"] = {"kernel": "skin16_kernel", "ms": ms["skin"], "bound": "hbm",
                            "achieved_GBs": a, "frac": a / PEAK_HBM_GBS,
-                           "in_timed_path": args.path == "unfused"}
+                           "bytes_per_hand": SKIN_BYTES_PER_HAND}
+    for k, v in kernels.items():
+        v["in_timed_path"] = k in in_path
 
     # Roofline of the dominant kernel of the timed path.
-    dominant = {"fused": "forward", "staged": "blend_skin"}.get(args.path)
-    if dominant is None:
+    if args.path == "unfused":
         dominant = "blend" if ms["blend"] >= ms["skin"] else "skin"
+    else:
+        dominant = "blend_skin"
     kd = kernels[dominant]
     if kd["bound"] == "mfma":
         roof = {"kernel": kd["kernel"], "bound": "mfma", "achieved": kd["achieved_TFLOPs"],
@@ -250,9 +253,8 @@ def main():
         roof = {"kernel": kd["kernel"], "bound": "hbm", "achieved": kd["achieved_GBs"],
                 "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": kd["frac"]}
     roof["traffic"] = load_traffic(args.pmc, dominant, B)
-    roof["algorithmic_per_hand"] = (FUSED_MFMA_FLOP_PER_HAND if dominant in ("forward", "blend_skin")
-                                    else BLEND_FLOP_PER_HAND if dominant == "blend"
-                                    else SKIN_BYTES_PER_HAND)
+    roof["algorithmic_per_hand"] = kd.get("flop_per_hand", kd.get("bytes_per_hand"))
+    roof["timed_in_region"] = dominant in in_path
 
     if rank == 0:
         total = B * world * args.steps

@@ -75,10 +75,10 @@ int mano_model_destroy(mano_model* model);
 /* Vertex count and device of a model. */
 int mano_model_info(const mano_model* model, int32_t* n_verts, int32_t* device);
 
-/* Device workspace (bytes) for n_hands that the mano_stage_* calls need
- * (`mano_workspace_bytes`; the unfused stages keep v_posed in it).
- * `mano_forward_workspace_bytes` is 0: mano_forward is a single launch that
- * keeps every intermediate on chip (its workspace arguments are ignored). */
+/* Device workspace (bytes) for n_hands: `mano_workspace_bytes` covers every
+ * call (the unfused stages keep v_posed in it); `mano_forward_workspace_bytes`
+ * only what mano_forward / articulate / blend_skin use (X rows + transforms,
+ * 1,408 B per hand). */
 size_t mano_workspace_bytes(const mano_model* model, int64_t n_hands);
 size_t mano_forward_workspace_bytes(const mano_model* model, int64_t n_hands);
 
@@ -91,11 +91,10 @@ int mano_workspace_offsets(const mano_model* model, int64_t n_hands,
                            size_t* vposed_off);
 
 /* The full forward pass: MANOModel.update() (mano_np.py:79-115) for n_hands
- * independent hands, one kernel launch (articulate + blend + skin fused; same
- * results as the staged calls bit for bit).  verts is required; joints,
- * rest_verts, rest_joints, rot_mats and trans are nullable; betas_stride 0
- * shares one beta row.  v_posed never touches HBM unless rest_verts is
- * requested.  workspace / workspace_bytes are unused (may be NULL / 0). */
+ * independent hands = articulate + blend_skin (two launches).  verts is
+ * required; joints, rest_verts, rest_joints, rot_mats and trans are nullable;
+ * betas_stride 0 shares one beta row.  v_posed never touches HBM unless
+ * rest_verts is requested. */
 int mano_forward(const mano_model* model, int64_t n_hands,
                  const float* betas, int64_t betas_stride, const float* pose,
                  const float* trans, float* verts, float* joints,

@@ -287,9 +287,8 @@ size_t mano_workspace_bytes(const mano_model* m, int64_t n) {
 }
 
 size_t mano_forward_workspace_bytes(const mano_model* m, int64_t n) {
-  (void)m;
-  (void)n;
-  return 0;  // mano_forward is one launch that keeps every intermediate on chip
+  if (check_model(m) || n < 0) return 0;
+  return mano::workspace_layout(m->dm, n).vposed_off;  // X rows + transforms
 }
 
 int mano_workspace_offsets(const mano_model* m, int64_t n, size_t* features_off,
@@ -385,22 +384,13 @@ int mano_forward(const mano_model* m, int64_t n, const float* betas, int64_t bet
                  const float* pose, const float* trans, float* verts, float* joints,
                  float* rest_verts, float* rest_joints, float* rot_mats, void* ws,
                  size_t ws_bytes, void* stream) {
-  (void)ws;
-  (void)ws_bytes;
+  g_last_error.clear();
   if (int rc = check_model(m)) return rc;
-  if (n < 0 || n > kMaxHands) return fail(MANO_EINVAL, "n_hands %lld out of range", (long long)n);
-  if (n == 0) return MANO_OK;
-  if (!verts) return fail(MANO_EINVAL, "verts is required");
-  if (!betas || !pose) return fail(MANO_EINVAL, "betas and pose are required");
-  if (betas_stride != 0 && betas_stride < mano::kShape)
-    return fail(MANO_EINVAL, "betas_stride %lld must be 0 or >= 10", (long long)betas_stride);
-  DeviceGuard guard(m->device);
-  if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
-  hipError_t e = mano::launch_forward(m->dm, n, betas, betas_stride, pose, trans, verts, joints,
-                                      rest_verts, rest_joints, rot_mats,
-                                      static_cast<hipStream_t>(stream));
-  if (e != hipSuccess) return hip_fail(e, "forward launch");
-  return MANO_OK;
+  if (n > 0 && !verts) return fail(MANO_EINVAL, "verts is required");
+  if (int rc = mano_stage_articulate(m, n, betas, betas_stride, pose, trans, joints, rest_joints,
+                                     rot_mats, ws, ws_bytes, stream))
+    return rc;
+  return mano_stage_blend_skin(m, n, rest_verts, trans, verts, ws, ws_bytes, stream);
 }
 
 int mano_pose_from_pca(const mano_model* m, int64_t n, const float* pca, int32_t n_comps,

@@ -94,11 +94,6 @@ hipError_t launch_blend(const DeviceModel& m, int64_t n, const float* features,
 hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features,
                              const float* transforms, const float* trans, float* verts,
                              float* vposed, hipStream_t stream);
-// The whole forward pass in one launch (articulation fused into blend_skin16).
-hipError_t launch_forward(const DeviceModel& m, int64_t n, const float* betas,
-                          int64_t betas_stride, const float* pose, const float* trans,
-                          float* verts, float* joints, float* vposed, float* rest_joints,
-                          float* rot_mats, hipStream_t stream);
 hipError_t launch_skin(const DeviceModel& m, int64_t n, const float* transforms,
                        const float* vposed, const float* trans, float* verts,
                        hipStream_t stream);

@@ -37,9 +37,9 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // the Taylor series to theta^4 is exact in float32.  Returning R - I (not R)
 // keeps the small pose features of :91 free of the cancellation too.
 //
-// Contraction is off in the articulation helpers: every kernel that inlines
-// them (articulate_kernel, the fused forward) must round identically, so the
-// staged and single-launch paths agree bit for bit; fmaf is spelled out.
+// Contraction is off in the articulation helpers and fmaf is spelled out, so
+// their rounding does not depend on how the compiler contracts the inlined
+// code (results are reproducible across builds and call sites).
 __device__ __forceinline__ void rodrigues_minus_eye(float x, float y, float z, float rm[9]) {
 #pragma clang fp contract(off)
   const float th2 = x * x + y * y + z * z;
@@ -155,14 +155,6 @@ __device__ __forceinline__ void store_joint_outputs(int64_t h, int j, const floa
 #pragma unroll
     for (int i = 0; i < 9; ++i) o[i] = rm[i] + ((i % 4 == 0) ? 1.f : 0.f);
   }
-}
-
-// Element k of hand row `hl` (0..15) of the blend GEMM A operand X in the
-// 16x16x4 fragment layout: step s = k / 4, lane hl + 16 (k & 3), packed as
-// [s / 4][64 lanes][s % 4] (the fused forward's LDS staging).
-__device__ __forceinline__ int x16_index(int hl, int k) {
-  const int s = k >> 2;
-  return (((s >> 2) * 64) + hl + 16 * (k & 3)) * 4 + (s & 3);
 }
 
 // ---------------------------------------------------------------------------
@@ -431,21 +423,6 @@ __device__ __forceinline__ void lbs_apply16_rows(const float (&F)[12][4], const 
   }
 }
 
-// Inputs of the articulation when the fused kernel computes it itself.
-struct ArticulateArgs {
-  const float* betas;
-  int64_t betas_stride;
-  const float* pose;
-  const float* joint_template;
-  const float* joint_shape;
-  const int32_t* parents;
-  const int32_t* depth;
-  int max_depth;
-  float* joints;
-  float* rest_joints;
-  float* rot_mats;
-};
-
 // Work split of the persistent launches: the (tile, vertex group) units are
 // cut into gridDim.x (blend_skin16: one range per block of 4 hand tiles) or
 // 4 gridDim.x (skin16: one range per wave) equal contiguous ranges, with the
@@ -457,27 +434,20 @@ __device__ __forceinline__ void unit_range(int64_t units, int64_t worker, int64_
   end = (worker + 1) * units / n_workers;
 }
 
-// kArticulate: the whole forward pass in one launch.  Each wave first
-// articulates its own 16 hands (4 passes of 4 hands x 16 joint lanes, the same
-// articulate_joint as articulate_kernel) and hands the results to its GEMM /
-// LBS lanes through a 12-KB LDS staging area -- first the features in
-// A-fragment order, then the transforms in LBS fragment order -- which the
-// basis tile ring re-uses afterwards.  Otherwise the A fragments and transforms are
-// read from the workspace written by articulate_kernel.
-//
-// A block owns a contiguous range of (quad of 4 hand tiles, vertex group)
-// units; at each quad it (re)builds its waves' operands, then runs that
-// quad's groups: 3 GEMM tiles (x, y, z) per group with the basis tiles staged
-// in LDS by LDS-DMA one tile ahead, then the LBS epilogue.
-template <bool kTrans, bool kArticulate>
+// Fused blend GEMM + LBS.  A block owns a contiguous range of (quad of 4
+// hand tiles, vertex group) units; at each quad its waves load their A
+// fragments (the X rows written by articulate_kernel) and LBS fragments (the
+// transforms), then run that quad's groups: 3 GEMM tiles (x, y, z) per group
+// with the basis tiles staged in LDS by LDS-DMA one tile ahead, then the LBS
+// epilogue on MFMA; v_posed never leaves registers.
+template <bool kTrans>
 __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
     const float* __restrict__ features, const float* __restrict__ transforms,
-    ArticulateArgs art, const float* __restrict__ basis16, const float* __restrict__ wfrag16,
+    const float* __restrict__ basis16, const float* __restrict__ wfrag16,
     const float* __restrict__ trans, float* __restrict__ verts, float* __restrict__ vposed,
     int64_t n, int n_verts, int n_groups) {
-  constexpr int kStageF4 = 12 * 64;          // 12 KB of staging per wave
-  constexpr int kRingF4 = kGroups16 * 64;    // one basis tile, 10 KB; ring of 2 at lds[0]
-  __shared__ f32x4 lds[kArticulate ? 4 * kStageF4 : 2 * kRingF4];
+  constexpr int kRingF4 = kGroups16 * 64;    // one basis tile, 10 KB; ring of 2
+  __shared__ f32x4 lds[2 * kRingF4];
   __shared__ float trs[4][16 * 3];  // the wave's 16 translations, read back at the stores
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int vstride32 = 3 * n_verts;
@@ -498,99 +468,25 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
     const int n_valid = active ? int(n - h0 < 16 ? n - h0 : 16) : 0;
 
     // An opaque lane index per range: keeps hipcc from hoisting lane-dependent
-    // addresses and loads (the 33 joint constants per lane, the staging
-    // offsets) out of the range loop, which would hold them in registers --
+    // addresses out of the range loop, which would hold them in registers --
     // spilled -- across the GEMM.
     int lane = threadIdx.x & 63;
     asm volatile("" : "+v"(lane));
     const int row0 = 4 * (lane >> 4);  // D rows (hands) of this lane: row0 + r
     const int col = lane & 15;         // D column (vertex of the group)
-    const float* jt = art.joint_template;
-    const float* js = art.joint_shape;
-    const int32_t* parents = art.parents;
-    const int32_t* depth = art.depth;
 
     float a[kGroups16 * 4];
     float F[12][4];  // LBS A fragments, tile (c, k) = c * 4 + k, resident for the quad
-    if constexpr (kArticulate) {
-      // (Every ring read of the previous range ended before its last barrier.)
-      float* stg = reinterpret_cast<float*>(lds + wave * kStageF4);
-      const f32x4* stg4 = lds + wave * kStageF4;
-      const int j = lane & 15;
-      const int par = parents[j];
-      const int dep = depth[j];
-      const int src = (lane & ~15) + (par < 0 ? 0 : par);
-      const int n_last = int(n - h0 < 16 ? n - h0 : 16) - 1;  // rows past the end repeat it
-      // All of the prologue's global loads first (one latency, not four).
-      float xyz[4][3], beta[4][kShape];
+    // A fragments from the X rows: lane's steps 4g..4g+3 are one dwordx4.
+    const int64_t row = min(h0 + (lane & 15), n - 1);
+    const f32x4* src = reinterpret_cast<const f32x4*>(features + row * kXStride) + (lane >> 4);
 #pragma unroll
-      for (int ps = 0; ps < 4; ++ps) {
-        const int64_t h = h0 + min(4 * ps + (lane >> 4), n_last);
+    for (int g = 0; g < kGroups16; ++g) {
+      const f32x4 v = src[4 * g];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) xyz[ps][c] = art.pose[h * (kJoints * 3) + 3 * j + c];
-#pragma unroll
-        for (int q = 0; q < kShape; ++q) beta[ps][q] = art.betas[h * art.betas_stride + q];
-      }
-      // Pass ps: lanes (hand 4 ps + (lane >> 4), joint lane & 15).  The
-      // features go to the staging area in A-fragment order right away; the
-      // transforms wait in registers until the features have been read back.
-      float Aj[4][12];
-#pragma unroll
-      for (int ps = 0; ps < 4; ++ps) {
-        const int hl = 4 * ps + (lane >> 4);
-        float rm[9], J[3], t[3];
-        articulate_joint(xyz[ps][0], xyz[ps][1], xyz[ps][2], beta[ps], j, src, dep, art.max_depth,
-                         jt, js, rm, J, t, Aj[ps]);
-        if (j == 0) {
-#pragma unroll
-          for (int q = 0; q < kShape; ++q) stg[x16_index(hl, q)] = beta[ps][q];
-          stg[x16_index(hl, kK)] = 1.f;  // X[:, 145] = 1 selects the template row
-#pragma unroll
-          for (int k = kK + 1; k < kGroups16 * 16; ++k) stg[x16_index(hl, k)] = 0.f;
-        } else {
-#pragma unroll
-          for (int m = 0; m < 9; ++m) stg[x16_index(hl, kShape + 9 * (j - 1) + m)] = rm[m];
-        }
-        if (g0 == 0 && hl < n_valid)  // the joint outputs come from the range holding group 0
-          store_joint_outputs(h0 + hl, j, trans, rm, J, t, art.joints, art.rest_joints,
-                              art.rot_mats);
-      }
-      __syncthreads();
-#pragma unroll
-      for (int g = 0; g < kGroups16; ++g) {
-        const f32x4 v = stg4[g * 64 + lane];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) a[4 * g + q] = v[q];
-      }
-      __syncthreads();
-      // LBS fragment order: F_{c,k}[q] of lane L = A_{4q + (L >> 4)}(hand L & 15)[c][k].
-#pragma unroll
-      for (int ps = 0; ps < 4; ++ps) {
-        const int hl = 4 * ps + (lane >> 4);
-#pragma unroll
-        for (int ck = 0; ck < 12; ++ck)
-          stg[(ck * 64 + hl + 16 * (j & 3)) * 4 + (j >> 2)] = Aj[ps][ck];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int ck = 0; ck < 12; ++ck) {
-        const f32x4 v = stg4[ck * 64 + lane];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) F[ck][q] = v[q];
-      }
-      __syncthreads();  // the basis ring overwrites the staging areas next
-    } else {
-      // A fragments from the X rows: lane's steps 4g..4g+3 are one dwordx4.
-      const int64_t row = min(h0 + (lane & 15), n - 1);
-      const f32x4* src = reinterpret_cast<const f32x4*>(features + row * kXStride) + (lane >> 4);
-#pragma unroll
-      for (int g = 0; g < kGroups16; ++g) {
-        const f32x4 v = src[4 * g];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) a[4 * g + q] = v[q];
-      }
-      load_lbs_frags(transforms, h0, n, lane, F);
+      for (int q = 0; q < 4; ++q) a[4 * g + q] = v[q];
     }
+    load_lbs_frags(transforms, h0, n, lane, F);
     if constexpr (kTrans) {
       if (lane < 48) {
         const int64_t h = h0 + lane / 3;
@@ -804,7 +700,7 @@ namespace {
 // kernel states the blocks per CU it is built for (its __launch_bounds__); the
 // occupancy API only caps that, because it reads one block per CU high for
 // kernels using 97-112 SGPRs on gfx950 (MI355X_MICROARCH.md, correctness
-// boundaries) -- the fused forward uses 106.
+// boundaries).
 constexpr int kBlendSkinBlocksPerCU = 3;  // 168 VGPRs
 constexpr int kSkinBlocksPerCU = 2;       // <= 256 VGPRs
 constexpr int kSkinDepth = 6;             // skin16 prefetch depth (groups)
@@ -830,41 +726,24 @@ dim3 persistent_grid(Kernel kernel, const DeviceModel& m, int64_t units, int wor
   return dim3{unsigned(blocks_wanted < cap ? blocks_wanted : cap)};
 }
 
-template <bool kTrans, bool kArticulate>
-hipError_t launch_blend_skin16(const DeviceModel& m, int64_t n, const float* features,
-                               const float* transforms, const ArticulateArgs& art,
-                               const float* trans, float* verts, float* vposed,
-                               hipStream_t stream) {
-  const int64_t n_quads = ((n + 15) / 16 + 3) / 4;
-  auto kernel = blend_skin16_kernel<kTrans, kArticulate>;
-  const dim3 grid = persistent_grid(kernel, m, n_quads * m.n_groups16, 1, kBlendSkinBlocksPerCU);
-  hipLaunchKernelGGL(kernel, grid, dim3(256), 0, stream, features, transforms, art, m.basis16,
-                     m.wfrag16, trans, verts, vposed, n, m.n_verts, m.n_groups16);
-  return hipGetLastError();
-}
-
 }  // namespace
 
 hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features,
                              const float* transforms, const float* trans, float* verts,
                              float* vposed, hipStream_t stream) {
-  const ArticulateArgs none{};
-  return trans ? launch_blend_skin16<true, false>(m, n, features, transforms, none, trans, verts,
-                                                   vposed, stream)
-               : launch_blend_skin16<false, false>(m, n, features, transforms, none, trans, verts,
-                                                    vposed, stream);
-}
-
-hipError_t launch_forward(const DeviceModel& m, int64_t n, const float* betas,
-                          int64_t betas_stride, const float* pose, const float* trans,
-                          float* verts, float* joints, float* vposed, float* rest_joints,
-                          float* rot_mats, hipStream_t stream) {
-  const ArticulateArgs art{betas, betas_stride, pose, m.joint_template, m.joint_shape, m.parents,
-                           m.depth, m.max_depth, joints, rest_joints, rot_mats};
-  return trans ? launch_blend_skin16<true, true>(m, n, nullptr, nullptr, art, trans, verts, vposed,
-                                                  stream)
-               : launch_blend_skin16<false, true>(m, n, nullptr, nullptr, art, trans, verts, vposed,
-                                                   stream);
+  const int64_t n_quads = ((n + 15) / 16 + 3) / 4;
+  if (trans) {
+    auto kernel = blend_skin16_kernel<true>;
+    hipLaunchKernelGGL(kernel, persistent_grid(kernel, m, n_quads * m.n_groups16, 1, kBlendSkinBlocksPerCU),
+                       dim3(256), 0, stream, features, transforms, m.basis16, m.wfrag16, trans,
+                       verts, vposed, n, m.n_verts, m.n_groups16);
+  } else {
+    auto kernel = blend_skin16_kernel<false>;
+    hipLaunchKernelGGL(kernel, persistent_grid(kernel, m, n_quads * m.n_groups16, 1, kBlendSkinBlocksPerCU),
+                       dim3(256), 0, stream, features, transforms, m.basis16, m.wfrag16, trans,
+                       verts, vposed, n, m.n_verts, m.n_groups16);
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_skin(const DeviceModel& m, int64_t n, const float* transforms,

@@ -85,7 +85,6 @@ class ManoHip:
             ctypes.byref(handle)))
         self._h = handle
         self._ws = None
-        self._ws_hands = -1
 
     # ------------------------------------------------------------------ utils
     def close(self):
@@ -108,16 +107,18 @@ class ManoHip:
                                                      ctypes.byref(c)))
         return a.value, b.value, c.value
 
-    def workspace(self, n: int) -> torch.Tensor:
-        """Cached device workspace large enough for `n` hands."""
-        if self._ws is None or self._ws_hands < n:
-            nbytes = max(self.workspace_bytes(n), 256)
-            self._ws = torch.empty(nbytes + 256, dtype=torch.uint8, device=self.device)
-            self._ws_hands = n
+    def workspace(self, n: int, forward_only: bool = False) -> torch.Tensor:
+        """Cached device workspace large enough for `n` hands (all stage calls,
+        or with `forward_only` just mano_forward's X rows + transforms)."""
+        lib = _abi.lib()
+        need = int(lib.mano_forward_workspace_bytes(self._h, n) if forward_only
+                   else lib.mano_workspace_bytes(self._h, n))
+        if self._ws is None or self._ws.numel() < need + 256:
+            self._ws = torch.empty(max(need, 256) + 256, dtype=torch.uint8, device=self.device)
         return self._ws
 
-    def _ws_args(self, n):
-        ws = self.workspace(n)
+    def _ws_args(self, n, forward_only: bool = False):
+        ws = self.workspace(n, forward_only)
         base = ws.data_ptr()
         aligned = (base + 255) & ~255
         return ctypes.c_void_p(aligned), ctypes.c_size_t(ws.numel() - (aligned - base))
@@ -180,10 +181,10 @@ class ManoHip:
         rv = buf("rest_verts", (B, V, 3), rest_verts)
         rj = buf("rest_joints", (B, N_JOINTS, 3), rest_joints)
         rm = buf("rot_mats", (B, N_JOINTS, 3, 3), rot_mats)
-        # One launch; mano_forward needs no workspace (mano_forward_workspace_bytes == 0).
+        ws, wsb = self._ws_args(B, forward_only=True)
         _abi.check(_abi.lib().mano_forward(
             self._h, B, _ptr(betas), bstride, _ptr(pose), _ptr(trans), _ptr(v), _ptr(j), _ptr(rv),
-            _ptr(rj), _ptr(rm), None, 0, _stream_handle(self.device, stream)))
+            _ptr(rj), _ptr(rm), ws, wsb, _stream_handle(self.device, stream)))
         return res
 
     # ---- the forward pass as separate kernels (per-kernel timing / intermediates) ----

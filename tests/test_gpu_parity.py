@@ -278,16 +278,20 @@ def test_errors(engine, dev):
                                    ctypes.c_void_p(p.data_ptr()), None, None, None, None,
                                    ctypes.c_void_p(ws.data_ptr()), 1024, None)
     assert rc == _abi.MANO_ESMALL and "workspace" in _abi.last_error()
-    # mano_forward needs no workspace; bad arguments are still refused
-    assert lib.mano_forward_workspace_bytes(engine._h, 64) == 0
+    # mano_forward: same workspace rule, bad arguments refused
+    need = lib.mano_forward_workspace_bytes(engine._h, 64)
+    assert 0 < need <= lib.mano_workspace_bytes(engine._h, 64)
     rc = lib.mano_forward(engine._h, 64, ctypes.c_void_p(b.data_ptr()), 10, ctypes.c_void_p(p.data_ptr()),
-                          None, ctypes.c_void_p(v.data_ptr()), None, None, None, None, None, 0, None)
-    assert rc == _abi.MANO_OK
+                          None, ctypes.c_void_p(v.data_ptr()), None, None, None, None,
+                          ctypes.c_void_p(ws.data_ptr()), 1024, None)
+    assert rc == _abi.MANO_ESMALL and "workspace" in _abi.last_error()
     rc = lib.mano_forward(engine._h, 64, ctypes.c_void_p(b.data_ptr()), 5, ctypes.c_void_p(p.data_ptr()),
-                          None, ctypes.c_void_p(v.data_ptr()), None, None, None, None, None, 0, None)
+                          None, ctypes.c_void_p(v.data_ptr()), None, None, None, None,
+                          ctypes.c_void_p(ws.data_ptr()), 1024, None)
     assert rc == _abi.MANO_EINVAL and "betas_stride" in _abi.last_error()
     rc = lib.mano_forward(engine._h, 64, ctypes.c_void_p(b.data_ptr()), 10, None, None,
-                          ctypes.c_void_p(v.data_ptr()), None, None, None, None, None, 0, None)
+                          ctypes.c_void_p(v.data_ptr()), None, None, None, None,
+                          ctypes.c_void_p(ws.data_ptr()), 1024, None)
     assert rc == _abi.MANO_EINVAL
     torch.cuda.synchronize()
 
@@ -337,8 +341,8 @@ def test_fused_equals_unfused(engine, dev, params, B):
 @pytest.mark.parametrize("B,shared,with_trans", [(1, False, True), (17, True, False),
                                                  (200, False, False), (4096, False, True)])
 def test_forward_equals_staged(engine, dev, params, B, shared, with_trans):
-    """The single-launch forward (articulation fused into blend_skin16) ==
-    articulate + blend_skin16 staged, bit for bit, for every output."""
+    """mano_forward == its two kernels called as stages (articulate, then
+    blend_skin16), bit for bit, for every output."""
     rng = np.random.default_rng(300 + B)
     betas = f32(rng.normal(0, 1, (10,) if shared else (B, 10)), dev)
     pose = f32(rng.normal(0, 0.6, (B, 16, 3)), dev)

@@ -13,17 +13,14 @@ import os
 import sys
 from collections import defaultdict
 
-# demangled-name prefix -> bench.py kernel key (the fused forward is the
-# blend_skin16 instantiation with the articulation prologue, <kTrans, true>)
-KERNELS = {"blend_skin16_kernel<false, true>": "forward", "blend_skin16_kernel<true, true>": "forward",
-           "blend_skin16_kernel<false, false>": "blend_skin",
-           "blend_skin16_kernel<true, false>": "blend_skin",
-           "blend_kernel(": "blend", "skin16_kernel<": "skin", "articulate_kernel(": "articulate"}
+# demangled-name prefix -> bench.py kernel key
+KERNELS = {"blend_skin16_kernel<": "blend_skin", "blend_kernel(": "blend", "skin16_kernel<": "skin",
+           "articulate_kernel(": "articulate"}
 # FETCH_SIZE correction (MI355X_MICROARCH.md §HBM): on gfx950 the counter
 # reports half the bytes of wide coalesced streams.  Measured here it is x2 for
 # every kernel of this path, dwordx3 streams included: skin16 raw 350.6 MB vs
 # 662 MB algorithmic reads, articulate raw 7.7 MB vs 15.2 MB (65,536 hands).
-FETCH_FACTOR = {"forward": 2.0, "blend_skin": 2.0, "blend": 2.0, "skin": 2.0, "articulate": 2.0}
+FETCH_FACTOR = {"blend_skin": 2.0, "blend": 2.0, "skin": 2.0, "articulate": 2.0}
 
 
 def short(name):
