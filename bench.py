@@ -35,7 +35,7 @@ SKIN_BYTES_PER_HAND = NCOL * 4 * 2 + 16 * 12 * 4   # v_posed in + verts out + tr
 SKIN_FLOP_PER_HAND = V * (16 * 12 * 2 + 9 * 2)     # blend 16 transforms + apply = 312,312
 LBS_T_FLOP_PER_HAND = V * 16 * 12 * 2              # the transform blend (on MFMA when fused) = 298,752
 FUSED_MFMA_FLOP_PER_HAND = BLEND_FLOP_PER_HAND + LBS_T_FLOP_PER_HAND  # 975,612
-ARTICULATE_BYTES_PER_HAND = (10 + 48) * 4 + 16 * 12 * 4 + 16 * 3 * 4 + 152 * 4  # in + A + joints + X
+ARTICULATE_BYTES_PER_HAND = (10 + 48) * 4 + 16 * 12 * 4 + 16 * 3 * 4 + 160 * 4  # in + A + joints + X row = 1,832
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, spec
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
