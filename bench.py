@@ -43,8 +43,12 @@ PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=20)
+    # The chip takes ~50 back-to-back launches (~30 ms) to reach its steady
+    # clock: blend_skin16 ran 0.73 ms -> 0.52 ms across the first 50 launches of
+    # a cold box (profiles/r01_kernel_trace_warmup.txt), so the default warmup
+    # is well past that.
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--batch", type=int, default=65536, help="hands per GPU per step")
     ap.add_argument("--gather", action="store_true", help="RCCL gather of verts+joints to GPU 0")
     ap.add_argument("--path", choices=("forward", "api", "unfused"), default="forward",
