@@ -16,8 +16,8 @@ def main():
         if not any(k in name for k in keys):
             continue
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-        short = name.split("(")[0].replace("mano::(anonymous namespace)::", "").replace("void ", "")
-        print(f"{short[:40]:40s} grid={r.get('Grid_Size_X', ''):>7s} us={d:8.1f} "
+        short = name.replace("mano::(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+        print(f"{short[:40]:40s} grid={r.get('Grid_Size_X', ''):>7s} us={d:.1f} "
               f"vgpr={r.get('VGPR_Count', '')} agpr={r.get('Accum_VGPR_Count', '')} "
               f"sgpr={r.get('SGPR_Count', '')} scratch={r.get('Scratch_Size', '')}")
 
