@@ -35,6 +35,7 @@ SKIN_BYTES_PER_HAND = NCOL * 4 * 2 + 16 * 12 * 4   # v_posed in + verts out + tr
 SKIN_FLOP_PER_HAND = V * (16 * 12 * 2 + 9 * 2)     # blend 16 transforms + apply = 312,312
 LBS_T_FLOP_PER_HAND = V * 16 * 12 * 2              # the transform blend (on MFMA when fused) = 298,752
 FUSED_MFMA_FLOP_PER_HAND = BLEND_FLOP_PER_HAND + LBS_T_FLOP_PER_HAND  # 975,612
+FUSED_BYTES_PER_HAND = 160 * 4 + 16 * 12 * 4 + NCOL * 4     # X row + transforms in, verts out = 10,744
 ARTICULATE_BYTES_PER_HAND = (10 + 48) * 4 + 16 * 12 * 4 + 16 * 3 * 4 + 160 * 4  # in + A + joints + X row = 1,832
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, spec
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -54,6 +55,9 @@ def parse():
     ap.add_argument("--path", choices=("forward", "api", "unfused"), default="forward",
                     help="forward: mano_forward's two kernels, each bracketed by events (default); "
                          "api: one mano_forward call per step; unfused: articulate + blend + skin")
+    ap.add_argument("--precision", choices=("fp32", "f16x3"), default="fp32",
+                    help="fp32: exact fp32 MFMA (default); f16x3: split-half MFMA "
+                         "(include/mano_hip.h MANO_PRECISION_F16X3)")
     ap.add_argument("--model", default=None, help="dump_model.py pickle (default: synthetic seed 0)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
@@ -115,7 +119,7 @@ def main():
     from mano_amd import ManoHip, load_dump, synthetic_params
     from mano_amd.distributed import gather_to_root
     params = load_dump(args.model) if args.model else synthetic_params(0)
-    model = ManoHip(params, device=local)
+    model = ManoHip(params, device=local, precision=args.precision)
 
     B = args.batch
     g = torch.Generator(device=dev).manual_seed(1001 + rank)
@@ -194,18 +198,26 @@ def main():
              "api": {"mano_forward": (0, 1)},
              "unfused": {"articulate": (0, 1), "blend": (1, 2), "skin": (2, 3)}}
     ms = {k: span(a, b, events) for k, (a, b) in timed[args.path].items()}
+    other = {"fp32": "f16x3", "f16x3": "fp32"}[args.precision]
+    ms_other = {}
     if rank == 0:
-        for path in ("forward", "api", "unfused"):
-            if path == args.path:
-                continue
+        def time_path(path, into, reps=50):
             evs = [[torch.cuda.Event(enable_timing=True) for _ in range(n_marks[path])]
-                   for _ in range(20)]
-            run_path(path)
+                   for _ in range(reps)]
+            for _ in range(reps):
+                run_path(path)
             for e in evs:
                 run_path(path, e)
             torch.cuda.synchronize()
             for k, (a, b) in timed[path].items():
-                ms.setdefault(k, span(a, b, evs))
+                into.setdefault(k, span(a, b, evs))
+        for path in ("forward", "api", "unfused"):
+            if path != args.path:
+                time_path(path, ms)
+        model.set_precision(other)
+        for path in ("forward", "unfused"):
+            time_path(path, ms_other)
+        model.set_precision(args.precision)
 
     def tflops(flop, t):
         return flop * B / (t * 1e-3) / 1e12
@@ -224,13 +236,19 @@ def main():
         kernels["articulate"] = {"kernel": "articulate_kernel", "ms": ms["articulate"],
                                  "bound": "latency", "achieved_GBs": a,
                                  "bytes_per_hand": ARTICULATE_BYTES_PER_HAND}
-    if "blend_skin" in ms:
+    if "blend_skin" in ms and args.precision == "fp32":
         a = tflops(FUSED_MFMA_FLOP_PER_HAND, ms["blend_skin"])
         kernels["blend_skin"] = {"kernel": "blend_skin16_kernel", "ms": ms["blend_skin"],
                                  "bound": "mfma", "achieved_TFLOPs": a,
                                  "frac": a / PEAK_FP32_TFLOPS,
                                  "flop_per_hand": FUSED_MFMA_FLOP_PER_HAND,
                                  "blend_gemm_TFLOPs": tflops(BLEND_FLOP_PER_HAND, ms["blend_skin"])}
+    elif "blend_skin" in ms:  # f16x3: the split GEMM runs at 16/3 x the fp32 rate; HBM stores bound it
+        a = gbs(FUSED_BYTES_PER_HAND, ms["blend_skin"])
+        kernels["blend_skin"] = {"kernel": "blend_skin_h3_kernel", "ms": ms["blend_skin"],
+                                 "bound": "hbm", "achieved_GBs": a, "frac": a / PEAK_HBM_GBS,
+                                 "bytes_per_hand": FUSED_BYTES_PER_HAND,
+                                 "fp32_equiv_TFLOPs": tflops(FUSED_MFMA_FLOP_PER_HAND, ms["blend_skin"])}
     if "blend" in ms:
         a = tflops(BLEND_FLOP_PER_HAND, ms["blend"])
         kernels["blend"] = {"kernel": "blend_kernel", "ms": ms["blend"], "bound": "mfma",
@@ -238,11 +256,30 @@ def main():
                             "flop_per_hand": BLEND_FLOP_PER_HAND}
     if "skin" in ms:
         a = gbs(SKIN_BYTES_PER_HAND, ms["skin"])
-        kernels["skin"] = {"kernel": "skin16_kernel", "ms": ms["skin"], "bound": "hbm",
+        kernels["skin"] = {"kernel": "skin16_kernel" if args.precision == "fp32" else "skin_h3_kernel",
+                           "ms": ms["skin"], "bound": "hbm",
                            "achieved_GBs": a, "frac": a / PEAK_HBM_GBS,
                            "bytes_per_hand": SKIN_BYTES_PER_HAND}
     for k, v in kernels.items():
         v["in_timed_path"] = k in in_path
+        v["precision"] = args.precision
+    # The other precision mode's kernels (timed after the timed region, not in `value`).
+    if "blend_skin" in ms_other:
+        t = ms_other["blend_skin"]
+        kernels[f"blend_skin_{other}"] = {
+            "kernel": "blend_skin_h3_kernel" if other == "f16x3" else "blend_skin16_kernel",
+            "ms": t, "precision": other, "in_timed_path": False,
+            "forward_hands_per_s": B / ((t + ms_other["articulate"]) * 1e-3),
+            "achieved_GBs": gbs(FUSED_BYTES_PER_HAND, t), "bytes_per_hand": FUSED_BYTES_PER_HAND,
+            "hbm_frac": gbs(FUSED_BYTES_PER_HAND, t) / PEAK_HBM_GBS,
+            "fp32_equiv_TFLOPs": tflops(FUSED_MFMA_FLOP_PER_HAND, t)}
+    if "skin" in ms_other:
+        t = ms_other["skin"]
+        kernels[f"skin_{other}"] = {
+            "kernel": "skin_h3_kernel" if other == "f16x3" else "skin16_kernel",
+            "ms": t, "precision": other, "in_timed_path": False, "bound": "hbm",
+            "achieved_GBs": gbs(SKIN_BYTES_PER_HAND, t),
+            "frac": gbs(SKIN_BYTES_PER_HAND, t) / PEAK_HBM_GBS, "bytes_per_hand": SKIN_BYTES_PER_HAND}
 
     # Roofline of the dominant kernel of the timed path.
     if args.path == "unfused":
@@ -273,7 +310,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": args.precision,
             "data": "synthetic (random-init MANO arrays of the official shapes, seed 0; "
                     "beta ~ N(0,1), pose ~ N(0,0.5^2) rad, generated on device)",
             "config": {"workload": "C2: full-pose fp32 MANO forward, 65,536 hands per GPU"

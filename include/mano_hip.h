@@ -50,6 +50,16 @@ extern "C" {
 #define MANO_N_POSE_FEATS 135
 #define MANO_N_PCA 45
 
+/* Arithmetic of the blend GEMM and LBS transform blend (mano_model_set_precision):
+ *  FP32   exact fp32 on v_mfma_f32_16x16x4_f32 (the default);
+ *  F16X3  every fp32 operand split into hi + lo halves (22 significant bits),
+ *         products hi.hi + hi.lo + lo.hi accumulated in fp32 on
+ *         v_mfma_f32_16x16x32_f16 (16/3 x the fp32 MFMA rate).  Same error
+ *         order as FP32 vs the float64 reference (~1e-7 m); needs |beta| and
+ *         the pose features within f16 range and skinning transforms < 1000. */
+#define MANO_PRECISION_FP32 0
+#define MANO_PRECISION_F16X3 1
+
 typedef struct mano_model mano_model; /* opaque, device-resident model buffer */
 
 /* Upload a model and build its device buffer.
@@ -68,6 +78,13 @@ int mano_model_create(int device, int32_t n_verts,
                       const double* skinning_weights, const int32_t* parents,
                       const double* pose_pca_basis, const double* pose_pca_mean,
                       mano_model** out);
+
+/* Select the arithmetic of mano_forward, mano_stage_blend_skin and
+ * mano_stage_skin on this handle (MANO_PRECISION_*; default FP32).  Not
+ * synchronised with launches already queued (they keep the mode they were
+ * issued with). */
+int mano_model_set_precision(mano_model* model, int32_t precision);
+int mano_model_get_precision(const mano_model* model, int32_t* precision);
 
 /* Free the device buffer.  NULL is accepted. */
 int mano_model_destroy(mano_model* model);

@@ -7,6 +7,7 @@
 // message.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -80,6 +81,41 @@ int check_workspace(const mano_model* m, int64_t n, const void* ws, size_t ws_by
 }
 
 constexpr int64_t kMaxHands = int64_t(1) << 30;
+
+// IEEE binary16 bits of a float, round to nearest even (host side of the
+// f16x3 operand split; overflow saturates to infinity, tiny values go
+// subnormal).
+uint16_t f16_bits(float f) {
+  uint32_t x;
+  std::memcpy(&x, &f, 4);
+  const uint32_t sign = (x >> 16) & 0x8000u;
+  const uint32_t absx = x & 0x7fffffffu;
+  if (absx >= 0x7f800000u) return uint16_t(sign | 0x7c00u | (absx > 0x7f800000u ? 0x200u : 0u));
+  if (absx >= 0x477ff000u) return uint16_t(sign | 0x7c00u);  // rounds past 65504
+  if (absx < 0x38800000u) {  // below the smallest normal half (2^-14): subnormal or zero
+    const float a = std::fabs(f) * 16777216.0f;  // units of 2^-24, exact scaling
+    const float r = std::nearbyint(a);           // default rounding mode: to nearest even
+    return uint16_t(sign | uint32_t(r));
+  }
+  const uint32_t mant = absx & 0x7fffffu;
+  uint32_t h = ((absx >> 23) - 112u) << 10 | (mant >> 13);
+  const uint32_t rest = mant & 0x1fffu;
+  if (rest > 0x1000u || (rest == 0x1000u && (h & 1u))) ++h;
+  return uint16_t(sign | h);
+}
+
+float f16_value(uint16_t h) {
+  const uint32_t e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+  float v = e == 0 ? std::ldexp(float(m), -24) : std::ldexp(float(m | 0x400u), int(e) - 25);
+  if (e == 31) v = m ? NAN : INFINITY;
+  return (h & 0x8000u) ? -v : v;
+}
+
+void split_f16(double x, uint16_t& hi, uint16_t& lo) {
+  const float xf = float(x);
+  hi = f16_bits(xf);
+  lo = f16_bits(xf - f16_value(hi));
+}
 
 }  // namespace
 
@@ -193,6 +229,44 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
           }
     }
   }
+  // f16x3 pieces (mano_internal.h): basis x 2^basis_exp with the largest
+  // entry at most 2^14, split hi/lo; weights x 2^kH3WeightExp.
+  double bmax = 0.0;
+  for (size_t i = 0; i < size_t(V) * 3 * kShape; ++i) bmax = std::max(bmax, std::fabs(mesh_shape_basis[i]));
+  for (size_t i = 0; i < size_t(V) * 3 * kPoseFeats; ++i) bmax = std::max(bmax, std::fabs(mesh_pose_basis[i]));
+  for (size_t i = 0; i < size_t(V) * 3; ++i) bmax = std::max(bmax, std::fabs(mesh_template[i]));
+  const int basis_exp = bmax > 0.0 ? 14 - int(std::ceil(std::log2(bmax))) : 0;
+  const double bscale = std::ldexp(1.0, basis_exp), wscale = std::ldexp(1.0, kH3WeightExp);
+  std::vector<uint16_t> bh3(size_t(n_groups16) * kH3GroupHalves, 0);
+  for (int g = 0; g < n_groups16; ++g) {
+    const int vb = std::max(0, std::min(16 * g, V - 16));
+    uint16_t* G = bh3.data() + size_t(g) * kH3GroupHalves;
+    for (int l = 0; l < 64; ++l) {
+      const int v = vb + (l & 15);
+      for (int j = 0; j < 8; ++j) {
+        const int kq = 8 * (l >> 4) + j;  // K index inside a 32-step
+        for (int c = 0; c < 3; ++c)
+          for (int s = 0; s < kH3Steps; ++s) {
+            const int k = 32 * s + kq;
+            double val = 0.0;
+            if (k <= kK && v < V) {
+              const size_t colv = size_t(v) * 3 + c;
+              val = k < kShape ? mesh_shape_basis[colv * kShape + k]
+                    : k < kK   ? mesh_pose_basis[colv * kPoseFeats + (k - kShape)]
+                               : mesh_template[colv];
+            }
+            uint16_t hi, lo;
+            split_f16(val * bscale, hi, lo);
+            G[(size_t((2 * c) * kH3Steps + s) * 64 + l) * 8 + j] = hi;
+            G[(size_t((2 * c + 1) * kH3Steps + s) * 64 + l) * 8 + j] = lo;
+          }
+        uint16_t hi, lo;
+        split_f16(skinning_weights[size_t(v) * kJoints + (kq & 15)] * wscale, hi, lo);
+        G[(size_t(kH3WPiece) * 64 + l) * 8 + j] = hi;                       // [Wh ; Wh]
+        G[(size_t(kH3WPiece + 1) * 64 + l) * 8 + j] = kq < 16 ? lo : 0;     // [Wl ; 0]
+      }
+    }
+  }
   std::vector<float> wts(size_t(V) * kJoints);
   for (size_t i = 0; i < wts.size(); ++i) wts[i] = float(skinning_weights[i]);
   std::vector<float> pca(kPca * kPca, 0.f), pmean(kPca, 0.f), zeros(64, 0.f);
@@ -203,7 +277,7 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
 
   // ---- one device block, 256-B aligned sub-arrays ----
   struct Part { const void* src; size_t bytes; size_t off; };
-  enum { kBasis, kWeights, kJt, kJs, kParents, kDepth, kPcaB, kPcaM, kZeros, kBasis16, kW16, kNParts };
+  enum { kBasis, kWeights, kJt, kJs, kParents, kDepth, kPcaB, kPcaM, kZeros, kBasis16, kW16, kBasisH3, kNParts };
   std::vector<Part> parts(kNParts);
   parts[kBasis] = {tiles.data(), tiles.size() * 4, 0};
   parts[kWeights] = {wts.data(), wts.size() * 4, 0};
@@ -216,6 +290,7 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   parts[kZeros] = {zeros.data(), zeros.size() * 4, 0};
   parts[kBasis16] = {b16.data(), b16.size() * 4, 0};
   parts[kW16] = {w16.data(), w16.size() * 4, 0};
+  parts[kBasisH3] = {bh3.data(), bh3.size() * 2, 0};
   size_t total = 0;
   for (auto& p : parts) {
     p.off = total;
@@ -252,6 +327,10 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   m->dm.zeros = at(kZeros);
   m->dm.basis16 = at(kBasis16);
   m->dm.wfrag16 = at(kW16);
+  m->dm.basis_h3 = reinterpret_cast<uint16_t*>(at(kBasisH3));
+  m->dm.h3_vposed_unscale = float(std::ldexp(1.0, -basis_exp));
+  m->dm.h3_lbs_unscale = float(std::ldexp(1.0, -(kH3FrameExp + kH3WeightExp)));
+  m->dm.precision = MANO_PRECISION_FP32;
   m->dm.n_groups16 = n_groups16;
   m->dm.max_depth = max_depth;
   m->dm.n_verts = V;
@@ -278,6 +357,22 @@ int mano_model_info(const mano_model* m, int32_t* n_verts, int32_t* device) {
   if (int rc = check_model(m)) return rc;
   if (n_verts) *n_verts = m->dm.n_verts;
   if (device) *device = m->device;
+  return MANO_OK;
+}
+
+int mano_model_set_precision(mano_model* m, int32_t precision) {
+  g_last_error.clear();
+  if (int rc = check_model(m)) return rc;
+  if (precision != MANO_PRECISION_FP32 && precision != MANO_PRECISION_F16X3)
+    return fail(MANO_EINVAL, "precision %d is not MANO_PRECISION_FP32 (0) or _F16X3 (1)", precision);
+  m->dm.precision = precision;
+  return MANO_OK;
+}
+
+int mano_model_get_precision(const mano_model* m, int32_t* precision) {
+  if (int rc = check_model(m)) return rc;
+  if (!precision) return fail(MANO_EINVAL, "precision is NULL");
+  *precision = m->dm.precision;
   return MANO_OK;
 }
 
@@ -354,8 +449,9 @@ int mano_stage_skin(const mano_model* m, int64_t n, const float* rest_verts, con
   const mano::Workspace w = mano::workspace_layout(m->dm, n);
   char* base = static_cast<char*>(ws);
   const float* vp = rest_verts ? rest_verts : reinterpret_cast<const float*>(base + w.vposed_off);
+  auto launch = m->dm.precision == MANO_PRECISION_F16X3 ? mano::launch_skin_h3 : mano::launch_skin;
   hipError_t e =
-      mano::launch_skin(m->dm, n, reinterpret_cast<const float*>(base + w.transforms_off), vp,
+      launch(m->dm, n, reinterpret_cast<const float*>(base + w.transforms_off), vp,
                         trans, verts, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "skin launch");
   return MANO_OK;
@@ -372,7 +468,9 @@ int mano_stage_blend_skin(const mano_model* m, int64_t n, float* rest_verts, con
   if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
   const mano::Workspace w = mano::workspace_layout(m->dm, n);
   char* base = static_cast<char*>(ws);
-  hipError_t e = mano::launch_blend_skin(
+  auto launch = m->dm.precision == MANO_PRECISION_F16X3 ? mano::launch_blend_skin_h3
+                                                          : mano::launch_blend_skin;
+  hipError_t e = launch(
       m->dm, n, reinterpret_cast<const float*>(base + w.features_off),
       reinterpret_cast<const float*>(base + w.transforms_off), trans, verts, rest_verts,
       static_cast<hipStream_t>(stream));

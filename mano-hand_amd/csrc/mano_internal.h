@@ -47,6 +47,32 @@ constexpr int kGroups16 = (kSteps16 + 3) / 4;  // 10 float4 groups per lane
 constexpr int kTile16Floats = kGroups16 * 64 * 4;   // 2560 floats = 10 KB
 constexpr int kWFrag16Floats = 64 * 4;         // 256 floats per 16-vertex group
 
+// f16x3 precision mode (mano_kernels_h3.hip): every fp32 operand x is carried
+// as an unevaluated pair of halves x = hi + lo (hi = f16(x), lo = f16(x - hi),
+// 22 significant bits) and each product as hi.hi + hi.lo + lo.hi on
+// v_mfma_f32_16x16x32_f16: the three partial products are exact in the fp32
+// accumulator, only lo.lo (< 2^-22 relative) is dropped.  Operands are scaled
+// by powers of two so their lo halves stay normal (scaling is exact).
+//   A operand of the blend GEMM: the X rows (unscaled), read from the same
+//     k-permuted fp32 rows the fp32 path uses and split in registers.
+//   B operand: the basis x 2^basis_exp, pre-split at model load into
+//     basis_h3[group][piece][64 lanes][8 halves], one 1-KB piece per
+//     (coord c, part hi/lo, K-step s of 32) = (2c + part) * 5 + s, pieces 30/31
+//     the LBS weight fragments [Wh ; Wh] and [Wl ; 0] (x 2^kH3WeightExp).
+//     Lane l of a K-step-s piece holds B[k = 32 s + 8 (l >> 4) + j][vertex
+//     vb + (l & 15)], j = 0..7 (the 16x16x32 operand map).
+//   LBS A operand: transforms x 2^kH3FrameExp, split per lane at load:
+//     lane l holds [Fh | Fl](hand l & 15)[k = 8 (l >> 4) + j] with k < 16 the
+//     hi halves of joints 0..15 and k >= 16 the lo halves, so
+//     [Fh | Fl] . [Wh ; Wh] + [Fh | Fl] . [Wl ; 0] = Fh Wh + Fl Wh + Fh Wl.
+constexpr int kH3Steps = 5;                          // K = 160 = 5 x 32
+constexpr int kH3PieceHalves = 64 * 8;               // one 1-KB fragment piece
+constexpr int kH3WPiece = 6 * kH3Steps;              // 30: [Wh ; Wh], 31: [Wl ; 0]
+constexpr int kH3GroupPieces = kH3WPiece + 2;        // 32 KB per 16-vertex group
+constexpr int kH3GroupHalves = kH3GroupPieces * kH3PieceHalves;
+constexpr int kH3FrameExp = 6;                       // transforms x 64 (|A| < 1000)
+constexpr int kH3WeightExp = 14;                     // weights x 16384 (|W| <= 1)
+
 // Device-resident model buffer (float32, layouts chosen for the kernels).
 struct DeviceModel {
   float* basis_tiles;   // [n_col_tiles][kKGroups][64][4] MFMA B fragments
@@ -60,6 +86,10 @@ struct DeviceModel {
   float* zeros;         // [64] zero vector (stand-in operand for an absent trans)
   float* basis16;       // [n_groups16][3][kTile16Floats]
   float* wfrag16;       // [n_groups16][kWFrag16Floats]
+  uint16_t* basis_h3;   // [n_groups16][kH3GroupHalves] f16 bits (f16x3 mode)
+  float h3_vposed_unscale;  // 2^-basis_exp: GEMM accumulator -> v_posed
+  float h3_lbs_unscale;     // 2^-(kH3FrameExp + kH3WeightExp): LBS sum -> verts
+  int32_t precision;    // MANO_PRECISION_* of mano_forward / blend_skin / skin
   int32_t max_depth;
   int32_t n_verts;
   int32_t n_cols;       // 3V
@@ -97,6 +127,14 @@ hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* featu
 hipError_t launch_skin(const DeviceModel& m, int64_t n, const float* transforms,
                        const float* vposed, const float* trans, float* verts,
                        hipStream_t stream);
+// f16x3 mode (mano_kernels_h3.hip): same operands and outputs as
+// launch_blend_skin / launch_skin.
+hipError_t launch_blend_skin_h3(const DeviceModel& m, int64_t n, const float* features,
+                                const float* transforms, const float* trans, float* verts,
+                                float* vposed, hipStream_t stream);
+hipError_t launch_skin_h3(const DeviceModel& m, int64_t n, const float* transforms,
+                          const float* vposed, const float* trans, float* verts,
+                          hipStream_t stream);
 hipError_t launch_pose_from_pca(const DeviceModel& m, int64_t n, const float* pca,
                                 int n_comps, int64_t pca_stride, const float* rot,
                                 int64_t rot_stride, float* pose, hipStream_t stream);

@@ -1,0 +1,371 @@
+// mano_kernels_h3.hip -- the f16x3 precision mode of the MANO forward pass on
+// gfx950 (MI355X): the blend GEMM (mano_np.py:81, :87-93) and the LBS
+// transform blend (:112) on v_mfma_f32_16x16x32_f16 with every fp32 operand
+// split into two halves (mano_internal.h, "f16x3 precision mode").
+//
+// gfx950 has no reduced-precision fast path for fp32 inputs (no xf32): an f32
+// MFMA runs at 1/16 of the f16 rate.  Three f16 MFMAs per product
+// (hi.hi + hi.lo + lo.hi, each exact in the fp32 accumulator) do the same
+// contraction at 16/3 x the f32 rate with 22 significant bits per operand:
+// measured vertex error vs the float64 reference is the same order as the
+// exact-fp32 path (~1e-7 m; tests/test_gpu_parity.py), and the forward pass
+// moves from the MFMA roof to the HBM store roof.
+//
+//   blend_skin_h3  fused: per (16-hand tile, 16-vertex group) 45 GEMM MFMAs
+//                  (3 coords x 5 K-steps x 3 split products) on basis pieces
+//                  LDS-DMA-staged per group (32 KB, ring of 2, shared by the 4
+//                  waves of a block), then 24 LBS MFMAs (12 transform tiles x
+//                  2) applied in registers; v_posed never leaves registers.
+//   skin_h3        standalone LBS over a v_posed buffer (HBM streaming), the
+//                  same 24 LBS MFMAs and apply order as blend_skin_h3.
+#include "mano_internal.h"
+
+namespace mano {
+namespace {
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x3 __attribute__((ext_vector_type(3)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x4 mfma_h(const f16x8& a, const f16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// Blend-GEMM A fragments of one hand row, split into halves.  Step s, element
+// j of lane quarter q = lane >> 4 is X[k = 32 s + 8 q + j]; in the k-permuted
+// fp32 row (x_pos) the pair (j = m, j = m + 4) sits at 16 (2 s + (q >> 1)) +
+// 4 m + 2 (q & 1), so each step is 4 dwordx2 loads.
+__device__ __forceinline__ void load_x_h3(const float* __restrict__ xrow, int q,
+                                          f16x8 (&xh)[kH3Steps], f16x8 (&xl)[kH3Steps]) {
+#pragma unroll
+  for (int s = 0; s < kH3Steps; ++s) {
+    const float* blk = xrow + 16 * (2 * s + (q >> 1)) + 2 * (q & 1);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const f32x2 v = *reinterpret_cast<const f32x2*>(blk + 4 * m);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const _Float16 h = static_cast<_Float16>(v[e]);
+        xh[s][m + 4 * e] = h;
+        xl[s][m + 4 * e] = static_cast<_Float16>(v[e] - static_cast<float>(h));
+      }
+    }
+  }
+}
+
+// LBS A fragments of a 16-hand tile from the [n][16][3][4] transforms:
+// F[c * 4 + k] element j of lane l = part(2^kH3FrameExp A_{8 ((l >> 4) & 1) + j}
+// (hand h0 + (l & 15))[c][k]), part = hi for l < 32, lo for l >= 32 (rows past
+// the batch end repeat the last hand).
+__device__ __forceinline__ void load_frames_h3(const float* __restrict__ transforms, int64_t h0,
+                                               int64_t n, int lane, f16x8 (&F)[12]) {
+  const int64_t n_left = n - 1 - h0;  // >= 0
+  const int hl = min(lane & 15, int(n_left < 15 ? n_left : 15));
+  const int q = lane >> 4;
+  const f32x4* A = reinterpret_cast<const f32x4*>(transforms + (h0 + hl) * kTransformFloats) +
+                   8 * (q & 1) * 3;
+  const bool lo = q >= 2;
+  constexpr float kScale = float(1 << kH3FrameExp);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const f32x4 v = A[3 * j + c];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float x = v[k] * kScale;
+        const _Float16 h = static_cast<_Float16>(x);
+        F[c * 4 + k][j] = lo ? static_cast<_Float16>(x - static_cast<float>(h)) : h;
+      }
+    }
+  }
+}
+
+// LBS of one 16-hand x 16-vertex tile (mano_np.py:112-115): transform tiles
+// T_{c,k} = [Fh | Fl].[Wh ; Wh] + [Fh | Fl].[Wl ; 0] (K = 32 each), applied to
+// the rest vertices p[coord] as out_c = fma(T_c3 + T_c2 z + T_c1 y + T_c0 x,
+// 2^-(kH3FrameExp + kH3WeightExp), trans_c), translation column first, every
+// rounding spelled out (fmaf) so fused and standalone LBS agree bit for bit.
+__device__ __forceinline__ void lbs_h3(const f16x8 (&F)[12], const f16x8& w1, const f16x8& w2,
+                                       const f32x4 (&p)[3], float t_unscale,
+                                       const float (&tr)[4][3], f32x4 (&out)[3]) {
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int k = 3 - kk;
+      f32x4 T = mfma_h(F[c * 4 + k], w2, f32x4{});
+      T = mfma_h(F[c * 4 + k], w1, T);
+      if (k == 3) {
+        out[c] = T;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[c][r] = fmaf(T[r], p[k][r], out[c][r]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[c][r] = fmaf(out[c][r], t_unscale, tr[r][c]);
+  }
+}
+
+// Workgroup barrier after s_waitcnt vmcnt(N) lgkmcnt(0): every vector-memory
+// op of this wave but the N youngest has completed (loads, stores and LDS-DMA
+// count together, in issue order) and every LDS access.  __syncthreads() would
+// add the workgroup release fence, i.e. vmcnt(0): a wait on the group's output
+// stores that the LDS hand-off does not need.
+template <int N>
+__device__ __forceinline__ void barrier_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void unit_range_h3(int64_t units, int64_t worker, int64_t n_workers,
+                                              int64_t& begin, int64_t& end) {
+  begin = worker * units / n_workers;
+  end = (worker + 1) * units / n_workers;
+}
+
+// One group's 32 fragment pieces (32 KB), global -> LDS, 8 pieces per wave.
+__device__ __forceinline__ void stage_group_h3(const uint16_t* __restrict__ basis_h3, int grp,
+                                               f16x8* slot, int wave, int lane) {
+  const uint16_t* src = basis_h3 + int64_t(grp) * kH3GroupHalves + lane * 8;
+#pragma unroll
+  for (int i = 0; i < kH3GroupPieces / 4; ++i) {
+    const int piece = wave + 4 * i;
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)(src + piece * kH3PieceHalves),
+        (__attribute__((address_space(3))) void*)(slot + piece * 64), 16, 0, 0);
+  }
+}
+
+// Fused blend GEMM + LBS, f16x3.  A block (4 waves, one 16-hand tile each)
+// owns a contiguous range of (quad of 4 hand tiles, vertex group) units; the
+// group's basis + weight pieces are LDS-DMA-staged once per block, one group
+// ahead (ring of 2 x 32 KB).  hipcc does not order LDS-DMA against the
+// barrier, so each group ends with an explicit vmcnt wait: the next group's
+// DMA was issued before this group's kStores output stores, so vmcnt(kStores)
+// covers it without waiting for the stores themselves.  Stores are branch-free
+// (rows past the batch end rewrite the last hand's identical values), so their
+// count is exact.
+template <bool kTrans, bool kVposed>
+__global__ __launch_bounds__(256, 2) void blend_skin_h3_kernel(
+    const float* __restrict__ features, const float* __restrict__ transforms,
+    const uint16_t* __restrict__ basis_h3, const float* __restrict__ trans,
+    float* __restrict__ verts, float* __restrict__ vposed, int64_t n, int n_verts, int n_groups,
+    float p_unscale, float t_unscale) {
+  constexpr int kSlot = kH3GroupPieces * 64;  // f16x8 per slot (32 KB)
+  constexpr int kStores = kVposed ? 8 : 4;    // global_store_dwordx3 per group
+  __shared__ f16x8 ring[2 * kSlot];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int vstride = 3 * n_verts;
+  const int64_t nt16 = (n + 15) / 16;
+  const int64_t n_quads = (nt16 + 3) / 4;
+  int64_t u, u_end;
+  unit_range_h3(n_quads * n_groups, blockIdx.x, gridDim.x, u, u_end);
+
+  while (u < u_end) {
+    const int64_t quad = u / n_groups;
+    const int g0 = int(u - quad * n_groups);
+    const int g1 = int(n_groups - g0 < u_end - u ? n_groups : g0 + (u_end - u));
+    u += g1 - g0;
+    // A wave past the batch end recomputes the last tile (identical values).
+    const int64_t h0 = min(quad * 4 + wave, nt16 - 1) * 16;
+    const int rmax = int(n - 1 - h0 < 15 ? n - 1 - h0 : 15);  // last row of the tile in the batch
+
+    int lane = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane));  // keep lane-derived addresses inside the range loop
+    const int q = lane >> 4;
+    const int col = lane & 15;
+
+    stage_group_h3(basis_h3, g0, ring + (g0 & 1) * kSlot, wave, lane);
+    f16x8 xh[kH3Steps], xl[kH3Steps], F[12];
+    load_x_h3(features + (h0 + min(col, rmax)) * kXStride, q, xh, xl);
+    load_frames_h3(transforms, h0, n, lane, F);
+    float tr[4][3] = {};
+    unsigned roff[4];  // this lane's D rows (hands 4q + r) in the tile, clamped to the batch
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int hr = min(4 * q + r, rmax);
+      roff[r] = unsigned(hr * vstride + 3 * col);
+      if constexpr (kTrans) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) tr[r][c] = trans[(h0 + hr) * 3 + c];
+      }
+    }
+    float* vtile = verts + h0 * int64_t(vstride);
+    float* ptile = kVposed ? vposed + h0 * int64_t(vstride) : nullptr;
+    __syncthreads();  // the first group's pieces (and the prologue loads) have landed
+
+    for (int grp = g0; grp < g1; ++grp) {
+      if (grp + 1 < g1) stage_group_h3(basis_h3, grp + 1, ring + ((grp + 1) & 1) * kSlot, wave, lane);
+      const f16x8* L = ring + (grp & 1) * kSlot + lane;
+      f32x4 p[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const f16x8* Bh = L + (2 * c) * kH3Steps * 64;
+        const f16x8* Bl = L + (2 * c + 1) * kH3Steps * 64;
+        f32x4 acc = {};
+#pragma unroll
+        for (int s = 0; s < kH3Steps; ++s) acc = mfma_h(xh[s], Bl[s * 64], acc);
+#pragma unroll
+        for (int s = 0; s < kH3Steps; ++s) acc = mfma_h(xl[s], Bh[s * 64], acc);
+#pragma unroll
+        for (int s = 0; s < kH3Steps; ++s) acc = mfma_h(xh[s], Bh[s * 64], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) p[c][r] = acc[r] * p_unscale;
+      }
+      const f16x8 w1 = L[kH3WPiece * 64];
+      const f16x8 w2 = L[(kH3WPiece + 1) * 64];
+      f32x4 out[3];
+      lbs_h3(F, w1, w2, p, t_unscale, tr, out);
+      const int voff = 3 * min(grp * 16, n_verts - 16);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        *reinterpret_cast<f32x3*>(vtile + (roff[r] + voff)) = f32x3{out[0][r], out[1][r], out[2][r]};
+        if constexpr (kVposed)
+          *reinterpret_cast<f32x3*>(ptile + (roff[r] + voff)) = f32x3{p[0][r], p[1][r], p[2][r]};
+      }
+      // Group grp + 1 has landed in LDS (every wave's pieces) and every wave
+      // is done reading slot grp & 1, which the next iteration re-stages.
+      barrier_vmcnt<kStores>();
+    }
+  }
+}
+
+// Standalone LBS, f16x3: each wave owns a contiguous range of (16-hand tile,
+// 16-vertex group) units (no LDS, no barriers); per tile the transform
+// fragments are built in VGPRs, per group the weight pieces and v_posed rows
+// are prefetched kDepth groups ahead in a register ring.
+template <bool kTrans, int kDepth>
+__global__ __launch_bounds__(256, 2) void skin_h3_kernel(
+    const float* __restrict__ transforms, const uint16_t* __restrict__ basis_h3,
+    const float* __restrict__ vposed, const float* __restrict__ trans, float* __restrict__ verts,
+    int64_t n, int n_verts, int n_groups, float t_unscale) {
+  const int lane = threadIdx.x & 63;
+  const int row0 = 4 * (lane >> 4);
+  const int col = lane & 15;
+  const int vstride = 3 * n_verts;
+  const int64_t nt16 = (n + 15) / 16;
+  int64_t u, u_end;
+  unit_range_h3(nt16 * n_groups, int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6),
+                int64_t(gridDim.x) * 4, u, u_end);
+  auto vbase = [&](int grp) { return 3 * min(grp * 16, n_verts - 16); };
+
+  while (u < u_end) {
+    const int64_t tile = u / n_groups;
+    const int g0 = int(u - tile * n_groups);
+    const int g1 = int(n_groups - g0 < u_end - u ? n_groups : g0 + (u_end - u));
+    u += g1 - g0;
+    const int64_t h0 = tile * 16;
+    const int n_valid = int(n - h0 < 16 ? n - h0 : 16);
+
+    f16x8 F[12];
+    load_frames_h3(transforms, h0, n, lane, F);
+    float tr[4][3] = {};
+    if constexpr (kTrans) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) tr[r][c] = trans[(h0 + min(row0 + r, n_valid - 1)) * 3 + c];
+    }
+    int roff[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) roff[r] = min(row0 + r, n_valid - 1) * vstride + 3 * col;
+    const float* ptile = vposed + h0 * int64_t(vstride);
+    float* vtile = verts + h0 * int64_t(vstride);
+    const f16x8* wsrc = reinterpret_cast<const f16x8*>(basis_h3) + lane;
+
+    auto load_p = [&](int grp, f32x3 (&pr)[4], f16x8& w1, f16x8& w2) {
+      const int g = min(grp, g1 - 1);
+      const float* src = ptile + vbase(g);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pr[r] = *reinterpret_cast<const f32x3*>(src + roff[r]);
+      const f16x8* wg = wsrc + int64_t(g) * (kH3GroupPieces * 64);
+      w1 = wg[kH3WPiece * 64];
+      w2 = wg[(kH3WPiece + 1) * 64];
+    };
+    f32x3 P[kDepth][4];
+    f16x8 W1[kDepth], W2[kDepth];
+#pragma unroll
+    for (int d = 0; d < kDepth; ++d) load_p(g0 + d, P[d], W1[d], W2[d]);
+    auto body = [&](int grp, f32x3 (&pr)[4], f16x8& w1, f16x8& w2) {
+      f32x4 p[3];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        p[0][r] = pr[r][0];
+        p[1][r] = pr[r][1];
+        p[2][r] = pr[r][2];
+      }
+      f32x4 out[3];
+      lbs_h3(F, w1, w2, p, t_unscale, tr, out);
+      load_p(grp + kDepth, pr, w1, w2);
+      const int vb = vbase(grp);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        *reinterpret_cast<f32x3*>(vtile + unsigned(roff[r] + vb)) = f32x3{out[0][r], out[1][r], out[2][r]};
+    };
+    int grp = g0;
+    for (; grp + kDepth <= g1; grp += kDepth) {
+#pragma unroll
+      for (int d = 0; d < kDepth; ++d) body(grp + d, P[d], W1[d], W2[d]);
+    }
+#pragma unroll
+    for (int d = 0; d < kDepth; ++d)
+      if (grp + d < g1) body(grp + d, P[d], W1[d], W2[d]);
+  }
+}
+
+constexpr int kBlendSkinH3BlocksPerCU = 2;  // 64 KB LDS ring per block
+constexpr int kSkinH3BlocksPerCU = 2;
+constexpr int kSkinH3Depth = 4;
+constexpr int64_t kMinUnitsPerWorkerH3 = 8;
+
+template <class Kernel>
+dim3 persistent_grid_h3(Kernel kernel, const DeviceModel& m, int64_t units, int workers_per_block,
+                        int design_per_cu) {
+  int b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, 256, 0) != hipSuccess || b < 1) b = 1;
+  if (b > design_per_cu) b = design_per_cu;
+  const int64_t cap = int64_t(b) * (m.n_cu > 0 ? m.n_cu : 1);
+  const int64_t want = (units + kMinUnitsPerWorkerH3 - 1) / kMinUnitsPerWorkerH3;
+  const int64_t blocks_wanted = (want + workers_per_block - 1) / workers_per_block;
+  return dim3{unsigned(blocks_wanted < cap ? blocks_wanted : cap)};
+}
+
+}  // namespace
+
+hipError_t launch_blend_skin_h3(const DeviceModel& m, int64_t n, const float* features,
+                                const float* transforms, const float* trans, float* verts,
+                                float* vposed, hipStream_t stream) {
+  const int64_t units = ((n + 15) / 16 + 3) / 4 * m.n_groups16;
+  auto launch = [&](auto kernel) {
+    hipLaunchKernelGGL(kernel, persistent_grid_h3(kernel, m, units, 1, kBlendSkinH3BlocksPerCU),
+                       dim3(256), 0, stream, features, transforms, m.basis_h3, trans, verts, vposed,
+                       n, m.n_verts, m.n_groups16, m.h3_vposed_unscale, m.h3_lbs_unscale);
+  };
+  if (trans && vposed) launch(blend_skin_h3_kernel<true, true>);
+  else if (trans) launch(blend_skin_h3_kernel<true, false>);
+  else if (vposed) launch(blend_skin_h3_kernel<false, true>);
+  else launch(blend_skin_h3_kernel<false, false>);
+  return hipGetLastError();
+}
+
+hipError_t launch_skin_h3(const DeviceModel& m, int64_t n, const float* transforms,
+                          const float* vposed, const float* trans, float* verts,
+                          hipStream_t stream) {
+  const int64_t units = (n + 15) / 16 * m.n_groups16;
+  if (trans) {
+    auto kernel = skin_h3_kernel<true, kSkinH3Depth>;
+    hipLaunchKernelGGL(kernel, persistent_grid_h3(kernel, m, units, 4, kSkinH3BlocksPerCU), dim3(256),
+                       0, stream, transforms, m.basis_h3, vposed, trans, verts, n, m.n_verts,
+                       m.n_groups16, m.h3_lbs_unscale);
+  } else {
+    auto kernel = skin_h3_kernel<false, kSkinH3Depth>;
+    hipLaunchKernelGGL(kernel, persistent_grid_h3(kernel, m, units, 4, kSkinH3BlocksPerCU), dim3(256),
+                       0, stream, transforms, m.basis_h3, vposed, trans, verts, n, m.n_verts,
+                       m.n_groups16, m.h3_lbs_unscale);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace mano

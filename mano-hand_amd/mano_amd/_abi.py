@@ -15,6 +15,8 @@ LIB_PATH = os.path.join(HERE, "libmano_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "mano_hip.h")
 
 MANO_OK, MANO_EINVAL, MANO_EHIP, MANO_ESMALL, MANO_ESTATE = 0, -1, -2, -3, -4
+MANO_PRECISION_FP32, MANO_PRECISION_F16X3 = 0, 1
+PRECISIONS = {"fp32": MANO_PRECISION_FP32, "f16x3": MANO_PRECISION_F16X3}
 _CODE_NAMES = {MANO_EINVAL: "MANO_EINVAL", MANO_EHIP: "MANO_EHIP",
                MANO_ESMALL: "MANO_ESMALL", MANO_ESTATE: "MANO_ESTATE"}
 
@@ -42,6 +44,8 @@ SIGNATURES = {
     "mano_model_create": (ctypes.c_int, [ctypes.c_int, _i32, _dptr, _dptr, _dptr, _dptr, _dptr,
                                          _ipt, _dptr, _dptr, ctypes.POINTER(_p)]),
     "mano_model_destroy": (ctypes.c_int, [_p]),
+    "mano_model_set_precision": (ctypes.c_int, [_p, _i32]),
+    "mano_model_get_precision": (ctypes.c_int, [_p, ctypes.POINTER(_i32)]),
     "mano_model_info": (ctypes.c_int, [_p, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
     "mano_workspace_bytes": (ctypes.c_size_t, [_p, _i64]),
     "mano_forward_workspace_bytes": (ctypes.c_size_t, [_p, _i64]),

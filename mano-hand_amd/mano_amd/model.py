@@ -49,7 +49,9 @@ X_POS = np.array([16 * (k >> 4) + 4 * (k & 3) + ((k >> 2) & 3) for k in range(X_
 class ManoHip:
     """Device-resident MANO model on one GPU (wraps a `mano_model*` handle)."""
 
-    def __init__(self, params: Dict[str, object], device=None):
+    def __init__(self, params: Dict[str, object], device=None, precision: str = "fp32"):
+        """`precision`: "fp32" (exact fp32 MFMA, default) or "f16x3" (split-half
+        MFMA, same error order; include/mano_hip.h MANO_PRECISION_*)."""
         check_layout(params)
         if device is None:
             idx = torch.cuda.current_device()
@@ -85,6 +87,14 @@ class ManoHip:
             ctypes.byref(handle)))
         self._h = handle
         self._ws = None
+        self.set_precision(precision)
+
+    def set_precision(self, precision: str) -> None:
+        """Arithmetic of forward / stage_blend_skin / stage_skin ("fp32" | "f16x3")."""
+        if precision not in _abi.PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(_abi.PRECISIONS)}, got {precision!r}")
+        _abi.check(_abi.lib().mano_model_set_precision(self._h, _abi.PRECISIONS[precision]))
+        self.precision = precision
 
     # ------------------------------------------------------------------ utils
     def close(self):

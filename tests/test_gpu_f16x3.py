@@ -1,0 +1,178 @@
+"""f16x3 precision mode (MANO_PRECISION_F16X3) vs the float64 oracle (MI355X only).
+
+The blend GEMM and the LBS transform blend run on v_mfma_f32_16x16x32_f16 with
+every fp32 operand split into hi + lo halves (mano_kernels_h3.hip).  The bar is
+the north_star tolerance, max |err| <= 1e-5 m on vertices and joints vs the
+float64 reference; the tests also assert TOL_FP32CLASS = 1e-6 m, an order
+below it, because the split keeps 22 significant bits per operand and the
+exact-fp32 path measures ~1e-7 m on the same inputs.
+"""
+import numpy as np
+import pytest
+
+from oracle import mano_oracle
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+TOL_M = 1e-5
+TOL_FP32CLASS = 1e-6
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def h3(params, dev):
+    from mano_amd import ManoHip
+    m = ManoHip(params, device=0, precision="f16x3")
+    yield m
+    m.close()
+
+
+def f32(a, dev):
+    return torch.tensor(np.asarray(a), dtype=torch.float32, device=dev)
+
+
+def host(t):
+    return t.double().cpu().numpy()
+
+
+def check(out, ref, where, tol=TOL_FP32CLASS):
+    ev = np.abs(host(out["verts"]) - ref["verts"]).max()
+    assert ev <= min(tol, TOL_M), f"{where}: verts max err {ev:.3e}"
+    if "joints" in out:
+        ej = np.abs(host(out["joints"]) - ref["joints"]).max()
+        assert ej <= min(tol, TOL_M), f"{where}: joints max err {ej:.3e}"
+    if "rest_verts" in out:
+        er = np.abs(host(out["rest_verts"]) - ref["rest_verts"]).max()
+        assert er <= min(tol, TOL_M), f"{where}: rest_verts max err {er:.3e}"
+    return ev
+
+
+def test_precision_switch(params, dev, h3):
+    from mano_amd import _abi
+    import ctypes
+    assert h3.precision == "f16x3"
+    got = ctypes.c_int32(-1)
+    _abi.check(_abi.lib().mano_model_get_precision(h3._h, ctypes.byref(got)))
+    assert got.value == _abi.MANO_PRECISION_F16X3
+    with pytest.raises(ValueError):
+        h3.set_precision("bf16")
+    assert _abi.lib().mano_model_set_precision(h3._h, 7) == _abi.MANO_EINVAL
+
+
+def test_golden_batch(h3, dev, golden_batch):
+    g = golden_batch
+    out = h3.forward(f32(g["betas"], dev), f32(g["pose"], dev), joints=True, rest_verts=True)
+    torch.cuda.synchronize()
+    check(out, {"verts": g["verts"], "joints": g["joints"], "rest_verts": g["rest_verts"]}, "golden")
+
+
+@pytest.mark.parametrize("B", [1, 2, 15, 16, 17, 63, 64, 65, 1000])
+def test_ragged_batches(h3, dev, params, B):
+    rng = np.random.default_rng(B)
+    betas = rng.normal(0, 1, (B, 10))
+    pose = rng.normal(0, 0.5, (B, 16, 3))
+    trans = rng.uniform(-1, 1, (B, 3))
+    out = h3.forward(f32(betas, dev), f32(pose, dev), f32(trans, dev), joints=True, rest_verts=True)
+    torch.cuda.synchronize()
+    check(out, mano_oracle.forward(params, betas, pose, trans), f"B={B}")
+
+
+@pytest.mark.parametrize("mag", [0.0, 1e-20, 1e-8, 1e-4, 1e-2, 0.1, np.pi, 2 * np.pi, 10.0])
+def test_edge_angles(h3, dev, params, mag):
+    rng = np.random.default_rng(17)
+    B = 64
+    d = rng.normal(size=(B, 16, 3))
+    d /= np.linalg.norm(d, axis=-1, keepdims=True)
+    pose = d * mag
+    betas = rng.normal(0, 1, (B, 10))
+    out = h3.forward(f32(betas, dev), f32(pose, dev), rest_verts=True)
+    torch.cuda.synchronize()
+    check(out, mano_oracle.forward(params, betas, pose), f"|theta|={mag}")
+
+
+def test_wide_inputs(h3, dev, params):
+    """Large shape coefficients and uniform [-pi, pi] poses stay fp32-class."""
+    rng = np.random.default_rng(3)
+    B = 512
+    pose = rng.uniform(-np.pi, np.pi, (B, 16, 3))
+    betas = rng.normal(0, 3, (B, 10))
+    betas[:8] = 10.0 * np.sign(rng.normal(size=(8, 10)))
+    out = h3.forward(f32(betas, dev), f32(pose, dev), rest_verts=True)
+    torch.cuda.synchronize()
+    check(out, mano_oracle.forward(params, betas, pose), "wide")
+
+
+def test_large_batch_sampled(h3, dev, params):
+    """C2 size: sampled hands vs the oracle, shard invariance, determinism."""
+    B = 65536
+    g = torch.Generator(device=dev).manual_seed(1001)
+    betas = torch.randn((B, 10), generator=g, device=dev)
+    pose = 0.5 * torch.randn((B, 16, 3), generator=g, device=dev)
+    trans = torch.rand((B, 3), generator=g, device=dev) * 2 - 1
+    out = h3.forward(betas, pose, trans, joints=True)
+    torch.cuda.synchronize()
+    verts = out["verts"]
+    assert torch.isfinite(verts).all()
+    idx = np.random.default_rng(0).choice(B, 256, replace=False)
+    idx = np.concatenate([idx, [0, 15, 16, 63, 64, B - 17, B - 1]])
+    ref = mano_oracle.forward(params, host(betas[idx]), host(pose[idx]), host(trans[idx]))
+    check({"verts": verts[idx], "joints": out["joints"][idx]}, ref, "C2 sampled")
+    for a, b in ((0, 1000), (1000, 40001), (40001, B)):
+        part = h3.forward(betas[a:b].contiguous(), pose[a:b].contiguous(), trans[a:b].contiguous())
+        assert torch.equal(part["verts"], verts[a:b])
+    again = h3.forward(betas, pose, trans)
+    assert torch.equal(again["verts"], verts)
+
+
+def test_matches_fp32_path(params, dev, h3):
+    """The two precision modes agree far inside the tolerance."""
+    from mano_amd import ManoHip
+    rng = np.random.default_rng(21)
+    B = 2048
+    betas = f32(rng.normal(0, 1, (B, 10)), dev)
+    pose = f32(rng.normal(0, 0.6, (B, 16, 3)), dev)
+    trans = f32(rng.uniform(-1, 1, (B, 3)), dev)
+    a = h3.forward(betas, pose, trans, rest_verts=True)
+    ref_engine = ManoHip(params, device=0)
+    b = ref_engine.forward(betas, pose, trans, rest_verts=True)
+    torch.cuda.synchronize()
+    ref_engine.close()
+    assert (a["verts"] - b["verts"]).abs().max().item() <= TOL_FP32CLASS
+    assert (a["rest_verts"] - b["rest_verts"]).abs().max().item() <= TOL_FP32CLASS
+
+
+@pytest.mark.parametrize("B", [1, 33, 200, 4096])
+def test_fused_lbs_equals_standalone(h3, dev, params, B):
+    """blend_skin_h3's LBS == skin_h3 on the v_posed it produced, bit for bit."""
+    rng = np.random.default_rng(100 + B)
+    betas = f32(rng.normal(0, 1, (B, 10)), dev)
+    pose = f32(rng.normal(0, 0.6, (B, 16, 3)), dev)
+    trans = f32(rng.uniform(-1, 1, (B, 3)), dev)
+    fused = h3.forward(betas, pose, trans, rest_verts=True)
+    v = torch.empty((B, 778, 3), device=dev)
+    h3.stage_articulate(betas, pose, trans)
+    h3.stage_skin(B, v, rest_verts=fused["rest_verts"], trans=trans)
+    torch.cuda.synchronize()
+    assert torch.equal(fused["verts"], v)
+    check({"verts": v}, mano_oracle.forward(params, host(betas), host(pose), host(trans)), f"B={B}")
+
+
+def test_standalone_skin_on_exact_vposed(h3, dev, params):
+    """skin_h3 over an exact-fp32 v_posed (the unfused blend kernel's) is fp32-class."""
+    rng = np.random.default_rng(5)
+    B = 777
+    betas = f32(rng.normal(0, 1, (B, 10)), dev)
+    pose = f32(rng.normal(0, 0.6, (B, 16, 3)), dev)
+    h3.stage_articulate(betas, pose)
+    vp = torch.empty((B, 778, 3), device=dev)
+    v = torch.empty((B, 778, 3), device=dev)
+    h3.stage_blend(B, rest_verts=vp)
+    h3.stage_skin(B, v, rest_verts=vp)
+    torch.cuda.synchronize()
+    check({"verts": v}, mano_oracle.forward(params, host(betas), host(pose)), "skin_h3")
