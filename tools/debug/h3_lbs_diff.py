@@ -7,7 +7,7 @@ from mano_amd import ManoHip, synthetic_params
 params = synthetic_params(0)
 m = ManoHip(params, device=0, precision="f16x3")
 dev = torch.device("cuda", 0)
-for B, with_trans in ((1, False), (1, True), (33, True)):
+for B, with_trans in ((1, False), (1, True), (33, True), (33, False), (200, True), (4096, True)):
     rng = np.random.default_rng(100 + B)
     f = lambda a: torch.tensor(a, dtype=torch.float32, device=dev)
     betas = f(rng.normal(0, 1, (B, 10))); pose = f(rng.normal(0, 0.6, (B, 16, 3)))
@@ -21,7 +21,8 @@ for B, with_trans in ((1, False), (1, True), (33, True)):
     bad = (d > 0).nonzero()
     print(B, with_trans, "max diff", d.max().item(), "n diff", bad.shape[0], "of", d.numel())
     if bad.shape[0]:
-        print("  first:", bad[:8].tolist(), "verts idx hist", torch.bincount(bad[:, 1] // 16).tolist()[:50])
+        print("  first:", bad[:8].tolist(), "group hist", torch.bincount(bad[:, 1] // 16).tolist()[:50])
+        print("  hand hist", torch.bincount(bad[:, 0]).tolist()[:64])
         print("  coord hist", torch.bincount(bad[:, 2]).tolist())
     from oracle import mano_oracle
     ref = mano_oracle.forward(params, betas.double().cpu().numpy(), pose.double().cpu().numpy(),
