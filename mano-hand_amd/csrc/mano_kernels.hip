@@ -17,10 +17,11 @@
 //                 MFMA, v_posed never leaving registers.
 //
 // The staged API adds the unfused kernels: blend (the same GEMM on
-// v_mfma_f32_32x32x2_f32, v_posed to HBM) and skin16 (HBM-streaming LBS with
-// the same MFMA transform tiles as blend_skin16, so both paths agree bit for
-// bit).
+// v_mfma_f32_32x32x2_f32, v_posed to HBM) and skin_span (HBM-streaming LBS
+// with the same MFMA transform tiles as blend_skin16, so both paths agree bit
+// for bit).
 #include "mano_internal.h"
+#include "mano_span.h"
 
 namespace mano {
 namespace {
@@ -425,7 +426,7 @@ __device__ __forceinline__ void lbs_apply16_rows(const float (&F)[12][4], const 
 
 // Work split of the persistent launches: the (tile, vertex group) units are
 // cut into gridDim.x (blend_skin16: one range per block of 4 hand tiles) or
-// 4 gridDim.x (skin16: one range per wave) equal contiguous ranges, with the
+// 4 gridDim.x (skin_span: one range per wave) equal contiguous ranges, with the
 // grid sized to the resident capacity of the chip, so every SIMD gets the same
 // MFMA / HBM work and there is no partially-filled second wave of blocks.
 __device__ __forceinline__ void unit_range(int64_t units, int64_t worker, int64_t n_workers,
@@ -542,100 +543,64 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// skin16: standalone LBS (mano_np.py:112-115) over a v_posed buffer, HBM
-// streaming.  Each wave owns a contiguous range of (16-hand tile, 16-vertex
-// group) units; per tile it loads the transform fragments into VGPRs, then
-// per group computes the same 12 v_mfma_f32_16x16x4_f32 transform tiles as
-// blend_skin16 (so both paths agree bit for bit) and applies them to v_posed,
-// which is prefetched kDepth groups ahead in a register ring (2 waves per SIMD
-// with ~18 KB of loads in flight each: HBM latency needs the bytes in flight
-// more than the extra waves).
+// skin_span: standalone LBS (mano_np.py:112-115) over a v_posed buffer, the
+// span streaming of mano_span.h (16 hands x 64 vertices per wave unit, whole-
+// line float4 sweeps through a per-wave LDS stage) with blend_skin16's LBS
+// operands and arithmetic: the transform fragments of a tile stay in VGPRs,
+// each group runs the same 12 v_mfma_f32_16x16x4_f32 transform tiles and
+// fmaf apply order (lbs_apply16_rows), then + trans -- so the staged path
+// agrees with blend_skin16 bit for bit.
 // ---------------------------------------------------------------------------
-template <bool kTrans, int kDepth>
-__global__ __launch_bounds__(256, 2) void skin16_kernel(
-    const float* __restrict__ transforms, const float* __restrict__ wfrag16,
-    const float* __restrict__ vposed, const float* __restrict__ trans,
-    float* __restrict__ verts, int64_t n, int n_verts, int n_groups) {
-  const int lane = threadIdx.x & 63;
-  const int row0 = 4 * (lane >> 4);
-  const int col = lane & 15;
-  const int vstride = 3 * n_verts;
-  const int64_t nt16 = (n + 15) / 16;
-  int64_t u, u_end;
-  unit_range(nt16 * n_groups, int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6), int64_t(gridDim.x) * 4,
-             u, u_end);
-  auto vbase = [&](int grp) { return 3 * min(grp * 16, n_verts - 16); };
-
-  while (u < u_end) {  // no barriers: each wave runs its own range
-    const int64_t tile = u / n_groups;
-    const int g0 = int(u - tile * n_groups);
-    const int g1 = int(n_groups - g0 < u_end - u ? n_groups : g0 + (u_end - u));
-    u += g1 - g0;
-    const int64_t h0 = tile * 16;
-    const int n_valid = int(n - h0 < 16 ? n - h0 : 16);
-
+template <bool kTrans>
+struct SpanLbs16 {
+  using W = f32x4;
+  struct Tile {
     float F[12][4];
-    load_lbs_frags(transforms, h0, n, lane, F);
-    float tr[4][3] = {};
+    float tr[4][3];
+  };
+  const float* transforms;
+  const float* wfrag16;
+  const float* trans;
+  Tile cur;
+
+  __device__ __forceinline__ W load_w(int grp, int lane) const {
+    return reinterpret_cast<const f32x4*>(wfrag16 + int64_t(grp) * kWFrag16Floats)[lane];
+  }
+  __device__ __forceinline__ void fetch_tile(int64_t h0, int64_t n, int n_valid, int lane, Tile& t) const {
+    load_lbs_frags(transforms, h0, n, lane, t.F);
     if constexpr (kTrans) {
+      const int row0 = 4 * (lane >> 4);
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int c = 0; c < 3; ++c) tr[r][c] = trans[(h0 + min(row0 + r, n_valid - 1)) * 3 + c];
+        for (int c = 0; c < 3; ++c) t.tr[r][c] = trans[(h0 + min(row0 + r, n_valid - 1)) * 3 + c];
     }
-    // Per-lane row offsets (rows past the batch end re-read the last hand).
-    int roff[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) roff[r] = min(row0 + r, n_valid - 1) * vstride + 3 * col;
-    const float* ptile = vposed + h0 * int64_t(vstride);
-    float* vtile = verts + h0 * int64_t(vstride);
-    // Group g's operands (rest vertices and the W fragment) are loaded kDepth
-    // groups ahead, so the wait before group g's MFMAs only covers loads that
-    // were issued kDepth - 1 groups earlier.  Each row's point is one dwordx3
-    // load kept as loaded (a register shuffle would wait on the prefetch).
-    auto load_p = [&](int grp, f32x3 (&p)[4], f32x4& wf) {
-      const int g = min(grp, g1 - 1);
-      const float* src = ptile + vbase(g);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) p[r] = *reinterpret_cast<const f32x3*>(src + roff[r]);
-      wf = reinterpret_cast<const f32x4*>(wfrag16 + int64_t(g) * kWFrag16Floats)[lane];
-    };
-    // Ring of kDepth register buffers: group g lives in slot g % kDepth and is
-    // re-loaded with group g + kDepth right after it is consumed.
-    f32x3 P[kDepth][4];
-    f32x4 W[kDepth];
-#pragma unroll
-    for (int d = 0; d < kDepth; ++d) load_p(g0 + d, P[d], W[d]);
-    auto body = [&](int grp, f32x3 (&p)[4], f32x4& wf) {
-      f32x4 out[3];
-      lbs_apply16_rows(F, wf, p, out);
-      load_p(grp + kDepth, p, wf);
-      // Branch-free stores: a row past the batch end holds the last hand's
-      // values and re-writes them (identical bits) to that hand's address.
-      const int vb = vbase(grp);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float* o = vtile + unsigned(roff[r] + vb);
-        float o0 = out[0][r], o1 = out[1][r], o2 = out[2][r];
-        if constexpr (kTrans) {
-          o0 += tr[r][0];
-          o1 += tr[r][1];
-          o2 += tr[r][2];
-        }
-        o[0] = o0;
-        o[1] = o1;
-        o[2] = o2;
-      }
-    };
-    int grp = g0;
-    for (; grp + kDepth <= g1; grp += kDepth) {
-#pragma unroll
-      for (int d = 0; d < kDepth; ++d) body(grp + d, P[d], W[d]);
-    }
-#pragma unroll
-    for (int d = 0; d < kDepth; ++d)
-      if (grp + d < g1) body(grp + d, P[d], W[d]);
   }
+  __device__ __forceinline__ void set_tile(const Tile& t) { cur = t; }
+  __device__ __forceinline__ void apply(const W& wf, const float (&p)[4][3], float (&o)[4][3]) const {
+    f32x3 pr[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pr[r] = f32x3{p[r][0], p[r][1], p[r][2]};
+    f32x4 out[3];
+    lbs_apply16_rows(cur.F, wf, pr, out);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) o[r][c] = kTrans ? out[c][r] + cur.tr[r][c] : out[c][r];
+  }
+};
+
+template <bool kTrans>
+__global__ __launch_bounds__(256, MANO_SPAN_BLOCKS_PER_CU) void skin_span_kernel(
+    const float* __restrict__ transforms, const float* __restrict__ wfrag16,
+    const float* __restrict__ vposed, const float* __restrict__ trans, float* __restrict__ verts,
+    int64_t n, int n_verts, int n_groups) {
+  __shared__ f32x4 stage[4 * span::kStageFloats / 4];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  SpanLbs16<kTrans> lbs{transforms, wfrag16, trans, {}};
+  span::run_units<true>(lbs, vposed, verts, n, n_verts, n_groups, span::xcd_worker(wave),
+                  int64_t(gridDim.x) * 4, reinterpret_cast<float*>(stage) + wave * span::kStageFloats,
+                  int(threadIdx.x & 63));
 }
 
 // ---------------------------------------------------------------------------
@@ -702,8 +667,7 @@ namespace {
 // kernels using 97-112 SGPRs on gfx950 (MI355X_MICROARCH.md, correctness
 // boundaries).
 constexpr int kBlendSkinBlocksPerCU = 3;  // 168 VGPRs
-constexpr int kSkinBlocksPerCU = 2;       // <= 256 VGPRs
-constexpr int kSkinDepth = 6;             // skin16 prefetch depth (groups)
+constexpr int kSkinBlocksPerCU = MANO_SPAN_BLOCKS_PER_CU;  // skin_span
 
 template <class Kernel>
 int64_t resident_blocks(Kernel kernel, const DeviceModel& m, int design_per_cu) {
@@ -749,16 +713,13 @@ hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* featu
 hipError_t launch_skin(const DeviceModel& m, int64_t n, const float* transforms,
                        const float* vposed, const float* trans, float* verts,
                        hipStream_t stream) {
-  const int64_t units = (n + 15) / 16 * m.n_groups16;
-  if (trans) {
-    auto kernel = skin16_kernel<true, kSkinDepth>;
-    hipLaunchKernelGGL(kernel, persistent_grid(kernel, m, units, 4, kSkinBlocksPerCU), dim3(256), 0, stream,
-                       transforms, m.wfrag16, vposed, trans, verts, n, m.n_verts, m.n_groups16);
-  } else {
-    auto kernel = skin16_kernel<false, kSkinDepth>;
-    hipLaunchKernelGGL(kernel, persistent_grid(kernel, m, units, 4, kSkinBlocksPerCU), dim3(256), 0, stream,
-                       transforms, m.wfrag16, vposed, trans, verts, n, m.n_verts, m.n_groups16);
-  }
+  const int64_t units = (n + 15) / 16 * span::n_spans(m.n_verts);
+  auto launch = [&](auto kernel) {
+    hipLaunchKernelGGL(kernel, persistent_grid(kernel, m, units, 4, kSkinBlocksPerCU), dim3(256), 0,
+                       stream, transforms, m.wfrag16, vposed, trans, verts, n, m.n_verts, m.n_groups16);
+  };
+  if (trans) launch(skin_span_kernel<true>);
+  else launch(skin_span_kernel<false>);
   return hipGetLastError();
 }
 

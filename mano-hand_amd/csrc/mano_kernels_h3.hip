@@ -16,8 +16,9 @@
 //                  LDS-DMA-staged per group (32 KB, ring of 2, shared by the 4
 //                  waves of a block), then 24 LBS MFMAs (12 transform tiles x
 //                  2) applied in registers; v_posed never leaves registers.
-//   skin_h3        standalone LBS over a v_posed buffer (HBM streaming), the
-//                  same 24 LBS MFMAs and apply order as blend_skin_h3.
+//   skin_span_h3   standalone LBS over a v_posed buffer (HBM streaming in
+//                  64-vertex spans, mano_span.h), the same 24 LBS MFMAs and
+//                  apply order as blend_skin_h3.
 //
 // Packed fp32 VALU (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32) is kept out of
 // these kernels: every scalar result the vectorizer could pair goes through
@@ -28,6 +29,7 @@
 // one of its source registers.  Packed fp32 beside MFMA is also the slower
 // form on gfx950 (MI355X_MICROARCH.md), so nothing is lost.
 #include "mano_internal.h"
+#include "mano_span.h"
 
 #ifndef MANO_H3_ASM_MFMA
 #define MANO_H3_ASM_MFMA 0
@@ -110,29 +112,40 @@ __device__ __forceinline__ void load_x_h3(const float* __restrict__ xrow, int q,
 // LBS A fragments of a 16-hand tile from the [n][16][3][4] transforms:
 // F[c * 4 + k] element j of lane l = part(2^kH3FrameExp A_{8 ((l >> 4) & 1) + j}
 // (hand h0 + (l & 15))[c][k]), part = hi for l < 32, lo for l >= 32 (rows past
-// the batch end repeat the last hand).
-__device__ __forceinline__ void load_frames_h3(const float* __restrict__ transforms, int64_t h0,
-                                               int64_t n, int lane, f16x8 (&F)[12]) {
+// the batch end repeat the last hand).  fetch: the lane's 8 joints x 3 rows;
+// split: the halves.
+__device__ __forceinline__ void fetch_frames_h3(const float* __restrict__ transforms, int64_t h0,
+                                                int64_t n, int lane, f32x4 (&raw)[24]) {
   const int64_t n_left = n - 1 - h0;  // >= 0
   const int hl = min(lane & 15, int(n_left < 15 ? n_left : 15));
-  const int q = lane >> 4;
   const f32x4* A = reinterpret_cast<const f32x4*>(transforms + (h0 + hl) * kTransformFloats) +
-                   8 * (q & 1) * 3;
-  const bool lo = q >= 2;
+                   8 * ((lane >> 4) & 1) * 3;
+#pragma unroll
+  for (int i = 0; i < 24; ++i) raw[i] = A[i];
+}
+
+__device__ __forceinline__ void split_frames_h3(const f32x4 (&raw)[24], int lane, f16x8 (&F)[12]) {
+  const bool lo = lane >= 32;
   constexpr float kScale = float(1 << kH3FrameExp);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      const f32x4 v = A[3 * j + c];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const float x = no_pack(v[k] * kScale);
+        const float x = no_pack(raw[3 * j + c][k] * kScale);
         const _Float16 h = static_cast<_Float16>(x);
         F[c * 4 + k][j] = lo ? static_cast<_Float16>(no_pack(x - static_cast<float>(h))) : h;
       }
     }
   }
+}
+
+__device__ __forceinline__ void load_frames_h3(const float* __restrict__ transforms, int64_t h0,
+                                               int64_t n, int lane, f16x8 (&F)[12]) {
+  f32x4 raw[24];
+  fetch_frames_h3(transforms, h0, n, lane, raw);
+  split_frames_h3(raw, lane, F);
 }
 
 // LBS of one 16-hand x 16-vertex tile (mano_np.py:112-115): transform tiles
@@ -298,93 +311,78 @@ __global__ __launch_bounds__(256, 2) void blend_skin_h3_kernel(
   }
 }
 
-// Standalone LBS, f16x3: each wave owns a contiguous range of (16-hand tile,
-// 16-vertex group) units (no LDS, no barriers); per tile the transform
-// fragments are built in VGPRs, per group the weight pieces and v_posed rows
-// are prefetched kDepth groups ahead in a register ring.
-template <bool kTrans, int kDepth>
-__global__ __launch_bounds__(256, 2) void skin_h3_kernel(
+// Standalone LBS, f16x3: the span streaming of mano_span.h with skin_h3's
+// operands -- the tile's split transform fragments in VGPRs, each group's
+// weight pieces from basis_h3 -- and lbs_h3 itself, so it agrees with
+// blend_skin_h3's LBS bit for bit.
+template <bool kTrans>
+struct SpanLbsH3 {
+  struct W {
+    f16x8 w1, w2;
+  };
+  struct Tile {
+    f32x4 raw[24];
+    float tr[4][3];
+  };
+  const float* transforms;
+  const uint16_t* basis_h3;
+  const float* trans;
+  float t_unscale;
+  int lane;
+  f16x8 F[12];
+  float tr[4][3];
+
+  __device__ __forceinline__ W load_w(int grp, int ln) const {
+    const f16x8* wg = reinterpret_cast<const f16x8*>(basis_h3) + int64_t(grp) * (kH3GroupPieces * 64) + ln;
+    return W{wg[kH3WPiece * 64], wg[(kH3WPiece + 1) * 64]};
+  }
+  __device__ __forceinline__ void fetch_tile(int64_t h0, int64_t n, int n_valid, int ln, Tile& t) const {
+    fetch_frames_h3(transforms, h0, n, ln, t.raw);
+    const int row0 = 4 * (ln >> 4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        t.tr[r][c] = kTrans ? trans[(h0 + min(row0 + r, n_valid - 1)) * 3 + c] : 0.f;
+  }
+  __device__ __forceinline__ void set_tile(const Tile& t) {
+    split_frames_h3(t.raw, lane, F);
+    operand_fence(F);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) tr[r][c] = t.tr[r][c];
+  }
+  __device__ __forceinline__ void apply(const W& w, const float (&p)[4][3], float (&o)[4][3]) const {
+    f32x4 pk[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pk[c][r] = p[r][c];
+    f32x4 out[3];
+    lbs_h3(F, w.w1, w.w2, pk, t_unscale, tr, out);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) o[r][c] = out[c][r];
+  }
+};
+
+template <bool kTrans>
+__global__ __launch_bounds__(256, MANO_SPAN_H3_BLOCKS_PER_CU) void skin_span_h3_kernel(
     const float* __restrict__ transforms, const uint16_t* __restrict__ basis_h3,
     const float* __restrict__ vposed, const float* __restrict__ trans, float* __restrict__ verts,
     int64_t n, int n_verts, int n_groups, float t_unscale) {
-  const int lane = threadIdx.x & 63;
-  const int row0 = 4 * (lane >> 4);
-  const int col = lane & 15;
-  const int vstride = 3 * n_verts;
-  const int64_t nt16 = (n + 15) / 16;
-  int64_t u, u_end;
-  unit_range_h3(nt16 * n_groups, int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6),
-                int64_t(gridDim.x) * 4, u, u_end);
-  auto vbase = [&](int grp) { return 3 * min(grp * 16, n_verts - 16); };
-
-  while (u < u_end) {
-    const int64_t tile = u / n_groups;
-    const int g0 = int(u - tile * n_groups);
-    const int g1 = int(n_groups - g0 < u_end - u ? n_groups : g0 + (u_end - u));
-    u += g1 - g0;
-    const int64_t h0 = tile * 16;
-    const int n_valid = int(n - h0 < 16 ? n - h0 : 16);
-
-    f16x8 F[12];
-    load_frames_h3(transforms, h0, n, lane, F);
-    operand_fence(F);
-    float tr[4][3] = {};
-    if constexpr (kTrans) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) tr[r][c] = trans[(h0 + min(row0 + r, n_valid - 1)) * 3 + c];
-    }
-    int roff[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) roff[r] = min(row0 + r, n_valid - 1) * vstride + 3 * col;
-    const float* ptile = vposed + h0 * int64_t(vstride);
-    float* vtile = verts + h0 * int64_t(vstride);
-    const f16x8* wsrc = reinterpret_cast<const f16x8*>(basis_h3) + lane;
-
-    auto load_p = [&](int grp, f32x3 (&pr)[4], f16x8& w1, f16x8& w2) {
-      const int g = min(grp, g1 - 1);
-      const float* src = ptile + vbase(g);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) pr[r] = *reinterpret_cast<const f32x3*>(src + roff[r]);
-      const f16x8* wg = wsrc + int64_t(g) * (kH3GroupPieces * 64);
-      w1 = wg[kH3WPiece * 64];
-      w2 = wg[(kH3WPiece + 1) * 64];
-    };
-    f32x3 P[kDepth][4];
-    f16x8 W1[kDepth], W2[kDepth];
-#pragma unroll
-    for (int d = 0; d < kDepth; ++d) load_p(g0 + d, P[d], W1[d], W2[d]);
-    auto body = [&](int grp, f32x3 (&pr)[4], f16x8& w1, f16x8& w2) {
-      f32x4 p[3];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        p[0][r] = pr[r][0];
-        p[1][r] = pr[r][1];
-        p[2][r] = pr[r][2];
-      }
-      f32x4 out[3];
-      lbs_h3(F, w1, w2, p, t_unscale, tr, out);
-      load_p(grp + kDepth, pr, w1, w2);
-      const int vb = vbase(grp);
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        *reinterpret_cast<f32x3*>(vtile + unsigned(roff[r] + vb)) = f32x3{out[0][r], out[1][r], out[2][r]};
-    };
-    int grp = g0;
-    for (; grp + kDepth <= g1; grp += kDepth) {
-#pragma unroll
-      for (int d = 0; d < kDepth; ++d) body(grp + d, P[d], W1[d], W2[d]);
-    }
-#pragma unroll
-    for (int d = 0; d < kDepth; ++d)
-      if (grp + d < g1) body(grp + d, P[d], W1[d], W2[d]);
-  }
+  __shared__ f32x4 stage[4 * span::kStageFloats / 4];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  SpanLbsH3<kTrans> lbs{transforms, basis_h3, trans, t_unscale, int(threadIdx.x & 63), {}, {}};
+  span::run_units<false>(lbs, vposed, verts, n, n_verts, n_groups, int64_t(blockIdx.x) * 4 + wave,
+                  int64_t(gridDim.x) * 4, reinterpret_cast<float*>(stage) + wave * span::kStageFloats,
+                  int(threadIdx.x & 63));
 }
 
 constexpr int kBlendSkinH3BlocksPerCU = 2;  // 64 KB LDS ring per block
-constexpr int kSkinH3BlocksPerCU = 2;
-constexpr int kSkinH3Depth = 3;
+constexpr int kSkinH3BlocksPerCU = MANO_SPAN_H3_BLOCKS_PER_CU;
 constexpr int64_t kMinUnitsPerWorkerH3 = 8;
 
 template <class Kernel>
@@ -420,18 +418,14 @@ hipError_t launch_blend_skin_h3(const DeviceModel& m, int64_t n, const float* fe
 hipError_t launch_skin_h3(const DeviceModel& m, int64_t n, const float* transforms,
                           const float* vposed, const float* trans, float* verts,
                           hipStream_t stream) {
-  const int64_t units = (n + 15) / 16 * m.n_groups16;
-  if (trans) {
-    auto kernel = skin_h3_kernel<true, kSkinH3Depth>;
+  const int64_t units = (n + 15) / 16 * span::n_spans(m.n_verts);
+  auto launch = [&](auto kernel) {
     hipLaunchKernelGGL(kernel, persistent_grid_h3(kernel, m, units, 4, kSkinH3BlocksPerCU), dim3(256),
                        0, stream, transforms, m.basis_h3, vposed, trans, verts, n, m.n_verts,
                        m.n_groups16, m.h3_lbs_unscale);
-  } else {
-    auto kernel = skin_h3_kernel<false, kSkinH3Depth>;
-    hipLaunchKernelGGL(kernel, persistent_grid_h3(kernel, m, units, 4, kSkinH3BlocksPerCU), dim3(256),
-                       0, stream, transforms, m.basis_h3, vposed, trans, verts, n, m.n_verts,
-                       m.n_groups16, m.h3_lbs_unscale);
-  }
+  };
+  if (trans) launch(skin_span_h3_kernel<true>);
+  else launch(skin_span_h3_kernel<false>);
   return hipGetLastError();
 }
 
