@@ -365,3 +365,44 @@ def test_forward_equals_staged(engine, dev, params, B, shared, with_trans):
                               None if trans is None else host(trans))
     assert np.abs(host(one["verts"]) - ref["verts"]).max() <= TOL_M
     assert np.abs(host(one["joints"]) - ref["joints"]).max() <= TOL_M
+
+
+def truncated_params(params, V):
+    """The synthetic model cut to its first V vertices: a smaller mesh of the
+    same layout (exercises every span / tail-group case of the kernels)."""
+    p = dict(params)
+    for k in ("mesh_template", "mesh_shape_basis", "mesh_pose_basis", "skinning_weights"):
+        p[k] = np.ascontiguousarray(np.asarray(params[k])[:V])
+    p["J_regressor"] = np.ascontiguousarray(np.asarray(params["J_regressor"])[:, :V])
+    f = np.asarray(params["faces"])
+    p["faces"] = f[(f < V).all(axis=1)]
+    return p
+
+
+@pytest.mark.parametrize("precision", ["fp32", "f16x3"])
+@pytest.mark.parametrize("V", [32, 50, 64, 100, 130, 200])
+def test_other_mesh_sizes(dev, params, V, precision):
+    """Meshes of V vertices: full 64-vertex spans (V // 64 of them) plus
+    1-4 tail groups, or tail groups only; fused == staged LBS bit for bit and
+    both within the tolerance of the oracle."""
+    from mano_amd import ManoHip
+    p = truncated_params(params, V)
+    m = ManoHip(p, device=0, precision=precision)
+    try:
+        B = 37
+        rng = np.random.default_rng(V)
+        betas = f32(rng.normal(0, 1, (B, 10)), dev)
+        pose = f32(rng.normal(0, 0.6, (B, 16, 3)), dev)
+        trans = f32(rng.uniform(-1, 1, (B, 3)), dev)
+        fused = m.forward(betas, pose, trans, joints=True, rest_verts=True)
+        m.stage_articulate(betas, pose, trans)
+        v = torch.empty((B, V, 3), device=dev)
+        m.stage_skin(B, v, rest_verts=fused["rest_verts"], trans=trans)
+        torch.cuda.synchronize()
+        assert torch.equal(fused["verts"], v)
+        ref = mano_oracle.forward(p, host(betas), host(pose), host(trans))
+        for key in ("verts", "joints", "rest_verts"):
+            err = np.abs(host(fused[key]) - ref[key]).max()
+            assert err <= TOL_M, (V, precision, key, err)
+    finally:
+        m.close()
