@@ -293,7 +293,7 @@ def main():
     else:
         roof = {"kernel": kd["kernel"], "bound": "hbm", "achieved": kd["achieved_GBs"],
                 "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": kd["frac"]}
-    roof["traffic"] = load_traffic(args.pmc, dominant, B)
+    roof["traffic"] = load_traffic(args.pmc, dominant + ("_h3" if args.precision == "f16x3" else ""), B)
     roof["algorithmic_per_hand"] = kd.get("flop_per_hand", kd.get("bytes_per_hand"))
     roof["timed_in_region"] = dominant in in_path
 

@@ -17,11 +17,13 @@ run() {  # name timeout args...
   echo "$name rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$OUT/$name.log"; exit $rc; fi
 }
-run stats 300 rocprofv3 --kernel-trace --stats -d $OUT/stats -o bench --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu
+# The default warmup (300 launches) so the averages are steady-clock ones, as in bench.py.
+run stats 400 rocprofv3 --kernel-trace --stats -d $OUT/stats -o bench --output-format csv -- python bench.py --no-cpu
 B="python bench.py --steps 5 --warmup 2 --no-cpu"
 run fetch 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o p --output-format csv -- $B
 run write 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o p --output-format csv -- $B
 run sq 300 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES -d $OUT/sq -o p --output-format csv -- $B
 run l2 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT TCC_HIT_sum TCC_MISS_sum -d $OUT/l2 -o p --output-format csv -- $B
+run waits 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS -d $OUT/waits -o p --output-format csv -- $B
 python tools/summarize_pmc.py $OUT > $OUT/summary.txt 2>&1; echo summarize rc=$?
 head -80 $OUT/summary.txt

@@ -14,13 +14,15 @@ import sys
 from collections import defaultdict
 
 # demangled-name prefix -> bench.py kernel key
-KERNELS = {"blend_skin16_kernel<": "blend_skin", "blend_kernel(": "blend", "skin16_kernel<": "skin",
-           "articulate_kernel(": "articulate"}
+KERNELS = {"blend_skin16_kernel<": "blend_skin", "blend_kernel(": "blend", "skin_span_kernel<": "skin",
+           "articulate_kernel(": "articulate", "blend_skin_h3_kernel<": "blend_skin_h3",
+           "skin_span_h3_kernel<": "skin_h3"}
 # FETCH_SIZE correction (MI355X_MICROARCH.md §HBM): on gfx950 the counter
 # reports half the bytes of wide coalesced streams.  Measured here it is x2 for
 # every kernel of this path, dwordx3 streams included: skin16 raw 350.6 MB vs
 # 662 MB algorithmic reads, articulate raw 7.7 MB vs 15.2 MB (65,536 hands).
-FETCH_FACTOR = {"blend_skin": 2.0, "blend": 2.0, "skin": 2.0, "articulate": 2.0}
+FETCH_FACTOR = {"blend_skin": 2.0, "blend": 2.0, "skin": 2.0, "articulate": 2.0,
+                "blend_skin_h3": 2.0, "skin_h3": 2.0}
 
 
 def short(name):
