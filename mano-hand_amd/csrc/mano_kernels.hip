@@ -462,11 +462,10 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
     const int g0 = int(u - quad * n_groups);
     const int g1 = int(n_groups - g0 < u_end - u ? n_groups : g0 + (u_end - u));
     u += g1 - g0;
-    const int64_t t16 = quad * 4 + wave;
-    const bool active = t16 < nt16;
-    const int64_t tc = active ? t16 : nt16 - 1;
-    const int64_t h0 = tc * 16;
-    const int n_valid = active ? int(n - h0 < 16 ? n - h0 : 16) : 0;
+    // A wave past the batch end recomputes the last tile and rewrites its
+    // (identical) values, so every store below is unconditional.
+    const int64_t h0 = min(quad * 4 + wave, nt16 - 1) * 16;
+    const int n_valid = int(n - h0 < 16 ? n - h0 : 16);
 
     // An opaque lane index per range: keeps hipcc from hoisting lane-dependent
     // addresses out of the range loop, which would hold them in registers --
@@ -516,27 +515,20 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
       const int voff = 3 * (vb + col);
       f32x4 out[3];
       lbs_apply16(F, wf, p, out);
+      // One 12-B point store per row; rows past the batch end rewrite the
+      // last hand's identical values.
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int hr = row0 + r;
-        if (hr < n_valid) {
-          float o0 = out[0][r], o1 = out[1][r], o2 = out[2][r];
-          if constexpr (kTrans) {
-            o0 += trs[wave][hr * 3 + 0];
-            o1 += trs[wave][hr * 3 + 1];
-            o2 += trs[wave][hr * 3 + 2];
-          }
-          float* o = vtile + unsigned(hr * vstride32 + voff);
-          o[0] = o0;
-          o[1] = o1;
-          o[2] = o2;
-          if (ptile) {
-            float* pv = ptile + unsigned(hr * vstride32 + voff);
-            pv[0] = p[0][r];
-            pv[1] = p[1][r];
-            pv[2] = p[2][r];
-          }
+        const int hr = min(row0 + r, n_valid - 1);
+        float o0 = out[0][r], o1 = out[1][r], o2 = out[2][r];
+        if constexpr (kTrans) {
+          o0 += trs[wave][hr * 3 + 0];
+          o1 += trs[wave][hr * 3 + 1];
+          o2 += trs[wave][hr * 3 + 2];
         }
+        *reinterpret_cast<f32x3*>(vtile + unsigned(hr * vstride32 + voff)) = f32x3{o0, o1, o2};
+        if (ptile)
+          *reinterpret_cast<f32x3*>(ptile + unsigned(hr * vstride32 + voff)) = f32x3{p[0][r], p[1][r], p[2][r]};
       }
     }
   }
