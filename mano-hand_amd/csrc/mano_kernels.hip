@@ -264,12 +264,18 @@ __device__ __forceinline__ void store_vposed_tile(float* __restrict__ vposed, co
   }
 }
 
+// The lane's byte offset is re-materialised at every call (an opaque 32-bit
+// value, so the source is SGPR base + VGPR offset): hoisted, hipcc kept a
+// 64-bit per-lane pointer live across the group loop and spilled it, and the
+// scratch reload's vmcnt(0) then waited for the previous group's stores.
 __device__ __forceinline__ void stage_basis_tile16(const float* __restrict__ basis16, int t,
                                                    f32x4* buf, int wave, int lane) {
-  const float* src = basis16 + int64_t(t) * kTile16Floats + lane * 4;
+  unsigned lane_off = unsigned(lane) * 16u;
+  asm volatile("" : "+v"(lane_off));
+  const char* src = reinterpret_cast<const char*>(basis16 + int64_t(t) * kTile16Floats);
   for (int g = wave; g < kGroups16; g += 4) {
     __builtin_amdgcn_global_load_lds(
-        (const __attribute__((address_space(1))) void*)(src + g * 256),
+        (const __attribute__((address_space(1))) void*)(src + (lane_off + unsigned(g) * 1024u)),
         (__attribute__((address_space(3))) void*)(buf + g * 64), 16, 0, 0);
   }
 }
