@@ -441,20 +441,40 @@ __device__ __forceinline__ void unit_range(int64_t units, int64_t worker, int64_
   end = (worker + 1) * units / n_workers;
 }
 
+// Workgroup barrier after s_waitcnt vmcnt(N) lgkmcnt(0): every vector-memory
+// op of this wave but the N youngest has completed (loads, stores and LDS-DMA
+// retire in issue order) and every LDS access.  __syncthreads() would wait
+// for vmcnt(0) -- the previous group's output stores too -- and hipcc does
+// not count the LDS-DMA as an LDS write.
+template <int N>
+__device__ __forceinline__ void barrier_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
 // Fused blend GEMM + LBS.  A block owns a contiguous range of (quad of 4
 // hand tiles, vertex group) units; at each quad its waves load their A
 // fragments (the X rows written by articulate_kernel) and LBS fragments (the
-// transforms), then run that quad's groups: 3 GEMM tiles (x, y, z) per group
-// with the basis tiles staged in LDS by LDS-DMA one tile ahead, then the LBS
-// epilogue on MFMA; v_posed never leaves registers.
-template <bool kTrans>
+// transforms), then run that quad's groups: 3 GEMM tiles (x, y, z) per group,
+// then the LBS epilogue on MFMA; v_posed never leaves registers.  The basis
+// tiles are LDS-DMA-staged two tiles ahead in a ring of 3 slots (tile q of a
+// group in slot q), so the barrier after tile t waits for tile t + 1's DMA
+// only: it was issued before the previous group's output stores, which stay
+// in flight (counted vmcnt, below).
+template <bool kTrans, bool kVposed>
 __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
     const float* __restrict__ features, const float* __restrict__ transforms,
     const float* __restrict__ basis16, const float* __restrict__ wfrag16,
     const float* __restrict__ trans, float* __restrict__ verts, float* __restrict__ vposed,
     int64_t n, int n_verts, int n_groups) {
-  constexpr int kRingF4 = kGroups16 * 64;    // one basis tile, 10 KB; ring of 2
-  __shared__ f32x4 lds[2 * kRingF4];
+  // One slot: a basis tile (10 KB) + the group's W fragment (1 KB, with the
+  // group's first tile); ring of 3.
+  constexpr int kRingF4 = (kGroups16 + 1) * 64;
+  constexpr int kStores = kVposed ? 8 : 4;   // global_store_dwordx3 per group
+  // vmcnt of the barrier after tile t: the wave's memory ops issued after tile
+  // t + 1's DMA -- tile t + 2's DMA (at least 2 pieces per wave) and, after a
+  // group's first tile, the previous group's stores.
+  constexpr int kPieces = kGroups16 / 4;     // LDS-DMA pieces per wave and tile, at least
+  __shared__ f32x4 lds[3 * kRingF4];
   __shared__ float trs[4][16 * 3];  // the wave's 16 translations, read back at the stores
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int vstride32 = 3 * n_verts;
@@ -500,22 +520,46 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
       }
     }
     float* vtile = verts + h0 * int64_t(vstride32);
-    float* ptile = vposed ? vposed + h0 * int64_t(vstride32) : nullptr;
-    const int t_end = 3 * g1;
+    float* ptile = kVposed ? vposed + h0 * int64_t(vstride32) : nullptr;
 
-    stage_basis_tile16(basis16, 3 * g0, lds + ((3 * g0) & 1) * kRingF4, wave, lane);
-    __syncthreads();
+    // The W fragment rides in the slot of the group's first tile (LDS-DMA by
+    // wave 2, which has the fewest basis pieces): a global load in the loop
+    // would make hipcc wait vmcnt(0) -- the tiles in flight -- before the LBS.
+    auto stage_w = [&](int grp, f32x4* slot) {
+      if (wave == 2) {
+        unsigned lane_off = unsigned(lane) * 16u;
+        asm volatile("" : "+v"(lane_off));
+        const char* src = reinterpret_cast<const char*>(wfrag16 + int64_t(grp) * kWFrag16Floats);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + lane_off),
+                                         (__attribute__((address_space(3))) void*)(slot + kGroups16 * 64),
+                                         16, 0, 0);
+      }
+    };
+    stage_basis_tile16(basis16, 3 * g0, lds, wave, lane);
+    stage_w(g0, lds);
+    stage_basis_tile16(basis16, 3 * g0 + 1, lds + kRingF4, wave, lane);
+    barrier_vmcnt<0>();  // the first two tiles and every prologue load have landed
 
     for (int grp = g0; grp < g1; ++grp) {
-      const f32x4 wf = reinterpret_cast<const f32x4*>(wfrag16 + int64_t(grp) * kWFrag16Floats)[lane];
+      const bool more = grp + 1 < g1;
       f32x4 p[3];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const int t = 3 * grp + q;
-        if (t + 1 < t_end) stage_basis_tile16(basis16, t + 1, lds + ((t + 1) & 1) * kRingF4, wave, lane);
-        p[q] = mfma16_tile(a, lds + (t & 1) * kRingF4, lane);
-        __syncthreads();
+      // Tile 3 grp + q in slot q; tile 3 grp + q + 2 goes to slot (q + 2) % 3.
+      stage_basis_tile16(basis16, 3 * grp + 2, lds + 2 * kRingF4, wave, lane);
+      const f32x4 wf = lds[kGroups16 * 64 + lane];  // read before slot 0 is re-staged
+      p[0] = mfma16_tile(a, lds, lane);
+      if (grp == g0) barrier_vmcnt<kPieces>();
+      else barrier_vmcnt<kPieces + kStores>();
+      if (more) {
+        stage_basis_tile16(basis16, 3 * grp + 3, lds, wave, lane);
+        stage_w(grp + 1, lds);
       }
+      p[1] = mfma16_tile(a, lds + kRingF4, lane);
+      if (more) barrier_vmcnt<kPieces>();
+      else barrier_vmcnt<0>();
+      if (more) stage_basis_tile16(basis16, 3 * grp + 4, lds + kRingF4, wave, lane);
+      p[2] = mfma16_tile(a, lds + 2 * kRingF4, lane);
+      if (more) barrier_vmcnt<kPieces>();
+      else barrier_vmcnt<0>();
       int vb = grp * 16;
       if (vb > n_verts - 16) vb = n_verts - 16;
       const int voff = 3 * (vb + col);
@@ -533,7 +577,7 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
           o2 += trs[wave][hr * 3 + 2];
         }
         *reinterpret_cast<f32x3*>(vtile + unsigned(hr * vstride32 + voff)) = f32x3{o0, o1, o2};
-        if (ptile)
+        if constexpr (kVposed)
           *reinterpret_cast<f32x3*>(ptile + unsigned(hr * vstride32 + voff)) = f32x3{p[0][r], p[1][r], p[2][r]};
       }
     }
@@ -694,17 +738,15 @@ hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* featu
                              const float* transforms, const float* trans, float* verts,
                              float* vposed, hipStream_t stream) {
   const int64_t n_quads = ((n + 15) / 16 + 3) / 4;
-  if (trans) {
-    auto kernel = blend_skin16_kernel<true>;
+  auto launch = [&](auto kernel) {
     hipLaunchKernelGGL(kernel, persistent_grid(kernel, m, n_quads * m.n_groups16, 1, kBlendSkinBlocksPerCU),
-                       dim3(256), 0, stream, features, transforms, m.basis16, m.wfrag16, trans,
-                       verts, vposed, n, m.n_verts, m.n_groups16);
-  } else {
-    auto kernel = blend_skin16_kernel<false>;
-    hipLaunchKernelGGL(kernel, persistent_grid(kernel, m, n_quads * m.n_groups16, 1, kBlendSkinBlocksPerCU),
-                       dim3(256), 0, stream, features, transforms, m.basis16, m.wfrag16, trans,
-                       verts, vposed, n, m.n_verts, m.n_groups16);
-  }
+                       dim3(256), 0, stream, features, transforms, m.basis16, m.wfrag16, trans, verts,
+                       vposed, n, m.n_verts, m.n_groups16);
+  };
+  if (trans && vposed) launch(blend_skin16_kernel<true, true>);
+  else if (trans) launch(blend_skin16_kernel<true, false>);
+  else if (vposed) launch(blend_skin16_kernel<false, true>);
+  else launch(blend_skin16_kernel<false, false>);
   return hipGetLastError();
 }
 
