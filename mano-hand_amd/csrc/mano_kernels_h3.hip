@@ -191,13 +191,18 @@ __device__ __forceinline__ void unit_range_h3(int64_t units, int64_t worker, int
   end = (worker + 1) * units / n_workers;
 }
 
-// One group's 32 fragment pieces (32 KB), global -> LDS, 8 pieces per wave.
+#ifndef MANO_H3_WAVES
+#define MANO_H3_WAVES 8
+#endif
+constexpr int kH3Waves = MANO_H3_WAVES;  // waves (16-hand tiles) per blend_skin_h3 block
+
+// One group's 32 fragment pieces (32 KB), global -> LDS, 32 / kH3Waves per wave.
 __device__ __forceinline__ void stage_group_h3(const uint16_t* __restrict__ basis_h3, int grp,
                                                f16x8* slot, int wave, int lane) {
   const uint16_t* src = basis_h3 + int64_t(grp) * kH3GroupHalves + lane * 8;
 #pragma unroll
-  for (int i = 0; i < kH3GroupPieces / 4; ++i) {
-    const int piece = wave + 4 * i;
+  for (int i = 0; i < kH3GroupPieces / kH3Waves; ++i) {
+    const int piece = wave + kH3Waves * i;
     __builtin_amdgcn_global_load_lds(
         (const __attribute__((address_space(1))) void*)(src + piece * kH3PieceHalves),
         (__attribute__((address_space(3))) void*)(slot + piece * 64), 16, 0, 0);
@@ -216,7 +221,7 @@ __device__ __forceinline__ void stage_group_h3(const uint16_t* __restrict__ basi
 // (rows past the batch end rewrite the last hand's identical values), so their
 // count is exact.
 template <bool kTrans, bool kVposed>
-__global__ __launch_bounds__(256, 2) void blend_skin_h3_kernel(
+__global__ __launch_bounds__(64 * kH3Waves, 8 / kH3Waves) void blend_skin_h3_kernel(
     const float* __restrict__ features, const float* __restrict__ transforms,
     const uint16_t* __restrict__ basis_h3, const float* __restrict__ trans,
     float* __restrict__ verts, float* __restrict__ vposed, int64_t n, int n_verts, int n_groups,
@@ -227,7 +232,7 @@ __global__ __launch_bounds__(256, 2) void blend_skin_h3_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int vstride = 3 * n_verts;
   const int64_t nt16 = (n + 15) / 16;
-  const int64_t n_quads = (nt16 + 3) / 4;
+  const int64_t n_quads = (nt16 + kH3Waves - 1) / kH3Waves;
   int64_t u, u_end;
   unit_range_h3(n_quads * n_groups, blockIdx.x, gridDim.x, u, u_end);
 
@@ -237,7 +242,7 @@ __global__ __launch_bounds__(256, 2) void blend_skin_h3_kernel(
     const int g1 = int(n_groups - g0 < u_end - u ? n_groups : g0 + (u_end - u));
     u += g1 - g0;
     // A wave past the batch end recomputes the last tile (identical values).
-    const int64_t h0 = min(quad * 4 + wave, nt16 - 1) * 16;
+    const int64_t h0 = min(quad * kH3Waves + wave, nt16 - 1) * 16;
     const int rmax = int(n - 1 - h0 < 15 ? n - 1 - h0 : 15);  // last row of the tile in the batch
 
     int lane = threadIdx.x & 63;
@@ -381,15 +386,15 @@ __global__ __launch_bounds__(256, MANO_SPAN_H3_BLOCKS_PER_CU) void skin_span_h3_
                   int(threadIdx.x & 63));
 }
 
-constexpr int kBlendSkinH3BlocksPerCU = 2;  // 64 KB LDS ring per block
+constexpr int kBlendSkinH3BlocksPerCU = 8 / kH3Waves;  // 64 KB LDS ring per block, 2 waves per SIMD
 constexpr int kSkinH3BlocksPerCU = MANO_SPAN_H3_BLOCKS_PER_CU;
 constexpr int64_t kMinUnitsPerWorkerH3 = 8;
 
 template <class Kernel>
 dim3 persistent_grid_h3(Kernel kernel, const DeviceModel& m, int64_t units, int workers_per_block,
-                        int design_per_cu) {
+                        int design_per_cu, int block_threads = 256) {
   int b = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, 256, 0) != hipSuccess || b < 1) b = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, block_threads, 0) != hipSuccess || b < 1) b = 1;
   if (b > design_per_cu) b = design_per_cu;
   const int64_t cap = int64_t(b) * (m.n_cu > 0 ? m.n_cu : 1);
   const int64_t want = (units + kMinUnitsPerWorkerH3 - 1) / kMinUnitsPerWorkerH3;
@@ -402,10 +407,10 @@ dim3 persistent_grid_h3(Kernel kernel, const DeviceModel& m, int64_t units, int 
 hipError_t launch_blend_skin_h3(const DeviceModel& m, int64_t n, const float* features,
                                 const float* transforms, const float* trans, float* verts,
                                 float* vposed, hipStream_t stream) {
-  const int64_t units = ((n + 15) / 16 + 3) / 4 * m.n_groups16;
+  const int64_t units = ((n + 15) / 16 + kH3Waves - 1) / kH3Waves * m.n_groups16;
   auto launch = [&](auto kernel) {
-    hipLaunchKernelGGL(kernel, persistent_grid_h3(kernel, m, units, 1, kBlendSkinH3BlocksPerCU),
-                       dim3(256), 0, stream, features, transforms, m.basis_h3, trans, verts, vposed,
+    hipLaunchKernelGGL(kernel, persistent_grid_h3(kernel, m, units, 1, kBlendSkinH3BlocksPerCU, 64 * kH3Waves),
+                       dim3(64 * kH3Waves), 0, stream, features, transforms, m.basis_h3, trans, verts, vposed,
                        n, m.n_verts, m.n_groups16, m.h3_vposed_unscale, m.h3_lbs_unscale);
   };
   if (trans && vposed) launch(blend_skin_h3_kernel<true, true>);

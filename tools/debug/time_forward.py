@@ -1,0 +1,33 @@
+"""Debug: time mano_forward's fused kernel (stage_blend_skin) of one library build, both precisions.
+
+    python tools/debug/time_forward.py [libmano_hip_<variant>.so]"""
+import os, sys
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [os.path.join(REPO, "mano-hand_amd"), REPO]
+import numpy as np, torch
+from mano_amd import _abi
+if len(sys.argv) > 1:
+    _abi.LIB_PATH = os.path.join(os.path.dirname(_abi.LIB_PATH), sys.argv[1])
+from mano_amd import ManoHip, synthetic_params
+B = 65536
+dev = torch.device("cuda", 0)
+g = torch.Generator(device=dev).manual_seed(3)
+betas = torch.randn((B, 10), generator=g, device=dev)
+pose = 0.5 * torch.randn((B, 16, 3), generator=g, device=dev)
+ref = None
+for prec in ("fp32", "f16x3"):
+    m = ManoHip(synthetic_params(0), device=0, precision=prec)
+    v = torch.empty((B, 778, 3), device=dev)
+    m.stage_articulate(betas, pose)
+    for _ in range(300):
+        m.stage_blend_skin(B, v)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(200)]
+    for a, b in ev:
+        a.record(); m.stage_blend_skin(B, v); b.record()
+    torch.cuda.synchronize()
+    ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if ref is None:
+        ref = v.clone()
+    err = (v - ref).abs().max().item()
+    print(f"{os.path.basename(_abi.LIB_PATH):24s} {prec:6s} blend_skin {ms:.4f} ms  vs fp32 max {err:.2e}", flush=True)
+    m.close()
