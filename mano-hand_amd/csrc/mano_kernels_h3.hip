@@ -195,6 +195,10 @@ __device__ __forceinline__ void unit_range_h3(int64_t units, int64_t worker, int
 #define MANO_H3_WAVES 8
 #endif
 constexpr int kH3Waves = MANO_H3_WAVES;  // waves (16-hand tiles) per blend_skin_h3 block
+#ifndef MANO_H3_GROUPS_PER_STAGE
+#define MANO_H3_GROUPS_PER_STAGE 1
+#endif
+constexpr int kH3GroupsPerStage = MANO_H3_GROUPS_PER_STAGE;  // vertex groups per barrier
 
 // One group's 32 fragment pieces (32 KB), global -> LDS, 32 / kH3Waves per wave.
 __device__ __forceinline__ void stage_group_h3(const uint16_t* __restrict__ basis_h3, int grp,
@@ -228,7 +232,7 @@ __global__ __launch_bounds__(64 * kH3Waves, 8 / kH3Waves) void blend_skin_h3_ker
     float p_unscale, float t_unscale) {
   constexpr int kSlot = kH3GroupPieces * 64;  // f16x8 per slot (32 KB)
   constexpr int kStores = kVposed ? 8 : 4;    // global_store_dwordx3 per group
-  __shared__ f16x8 ring[2 * kSlot];
+  __shared__ f16x8 ring[2 * kH3GroupsPerStage * kSlot];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int vstride = 3 * n_verts;
   const int64_t nt16 = (n + 15) / 16;
@@ -250,7 +254,13 @@ __global__ __launch_bounds__(64 * kH3Waves, 8 / kH3Waves) void blend_skin_h3_ker
     const int q = lane >> 4;
     const int col = lane & 15;
 
-    stage_group_h3(basis_h3, g0, ring + (g0 & 1) * kSlot, wave, lane);
+    // Stages of kH3GroupsPerStage groups, double-buffered: stage st holds
+    // groups [gb, ge) in slots st * kH3GroupsPerStage + i.
+    auto stage_groups = [&](int gb, int ge, int st) {
+      for (int i = 0; i < kH3GroupsPerStage; ++i)
+        if (gb + i < ge) stage_group_h3(basis_h3, gb + i, ring + (st * kH3GroupsPerStage + i) * kSlot, wave, lane);
+    };
+    stage_groups(g0, min(g0 + kH3GroupsPerStage, g1), 0);
     f16x8 xh[kH3Steps], xl[kH3Steps], F[12];
     load_x_h3(features + (h0 + min(col, rmax)) * kXStride, q, xh, xl);
     load_frames_h3(transforms, h0, n, lane, F);
@@ -273,45 +283,53 @@ __global__ __launch_bounds__(64 * kH3Waves, 8 / kH3Waves) void blend_skin_h3_ker
     // The first group's pieces and every prologue load have landed.
     barrier_vmcnt<0>();
 
-    for (int grp = g0; grp < g1; ++grp) {
-      if (grp + 1 < g1) stage_group_h3(basis_h3, grp + 1, ring + ((grp + 1) & 1) * kSlot, wave, lane);
-      const f16x8* L = ring + (grp & 1) * kSlot + lane;
-      // The three coordinates' chains interleaved (independent accumulators),
-      // each summing hi.lo, lo.hi, then hi.hi over the 5 K-steps.
-      f32x4 p[3];
+    for (int gb = g0, st = 0; gb < g1; gb += kH3GroupsPerStage, st ^= 1) {
+      const int ge = min(gb + kH3GroupsPerStage, g1);
+      if (ge < g1) stage_groups(ge, min(ge + kH3GroupsPerStage, g1), st ^ 1);
 #pragma unroll
-      for (int c = 0; c < 3; ++c) mfma_init(p[c], xh[0], L[((2 * c + 1) * kH3Steps) * 64]);
+      for (int i = 0; i < kH3GroupsPerStage; ++i) {
+        const int grp = gb + i;
+        if (grp >= ge) break;
+        const f16x8* L = ring + (st * kH3GroupsPerStage + i) * kSlot + lane;
+        // The three coordinates' chains interleaved (independent accumulators),
+        // each summing hi.lo, lo.hi, then hi.hi over the 5 K-steps.
+        f32x4 p[3];
 #pragma unroll
-      for (int s = 1; s < kH3Steps; ++s)
+        for (int c = 0; c < 3; ++c) mfma_init(p[c], xh[0], L[((2 * c + 1) * kH3Steps) * 64]);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) mfma_acc(p[c], xh[s], L[((2 * c + 1) * kH3Steps + s) * 64]);
+        for (int s = 1; s < kH3Steps; ++s)
 #pragma unroll
-      for (int s = 0; s < kH3Steps; ++s)
+          for (int c = 0; c < 3; ++c) mfma_acc(p[c], xh[s], L[((2 * c + 1) * kH3Steps + s) * 64]);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) mfma_acc(p[c], xl[s], L[((2 * c) * kH3Steps + s) * 64]);
+        for (int s = 0; s < kH3Steps; ++s)
 #pragma unroll
-      for (int s = 0; s < kH3Steps; ++s)
+          for (int c = 0; c < 3; ++c) mfma_acc(p[c], xl[s], L[((2 * c) * kH3Steps + s) * 64]);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) mfma_acc(p[c], xh[s], L[((2 * c) * kH3Steps + s) * 64]);
-      mfma_fence(p);
+        for (int s = 0; s < kH3Steps; ++s)
 #pragma unroll
-      for (int c = 0; c < 3; ++c)
+          for (int c = 0; c < 3; ++c) mfma_acc(p[c], xh[s], L[((2 * c) * kH3Steps + s) * 64]);
+        mfma_fence(p);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) p[c][r] = no_pack(p[c][r] * p_unscale);
-      const int voff = 3 * min(grp * 16, n_verts - 16);
-      const f16x8 w1 = L[kH3WPiece * 64];
-      const f16x8 w2 = L[(kH3WPiece + 1) * 64];
-      f32x4 out[3];
-      lbs_h3(F, w1, w2, p, t_unscale, tr, out);
+        for (int c = 0; c < 3; ++c)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        *reinterpret_cast<f32x3*>(vtile + (roff[r] + voff)) = f32x3{out[0][r], out[1][r], out[2][r]};
-        if constexpr (kVposed)
-          *reinterpret_cast<f32x3*>(ptile + (roff[r] + voff)) = f32x3{p[0][r], p[1][r], p[2][r]};
+          for (int r = 0; r < 4; ++r) p[c][r] = no_pack(p[c][r] * p_unscale);
+        const int voff = 3 * min(grp * 16, n_verts - 16);
+        const f16x8 w1 = L[kH3WPiece * 64];
+        const f16x8 w2 = L[(kH3WPiece + 1) * 64];
+        f32x4 out[3];
+        lbs_h3(F, w1, w2, p, t_unscale, tr, out);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          *reinterpret_cast<f32x3*>(vtile + (roff[r] + voff)) = f32x3{out[0][r], out[1][r], out[2][r]};
+          if constexpr (kVposed)
+            *reinterpret_cast<f32x3*>(ptile + (roff[r] + voff)) = f32x3{p[0][r], p[1][r], p[2][r]};
+        }
       }
-      // Group grp + 1 has landed in LDS (every wave's pieces) and every wave
-      // is done reading slot grp & 1, which the next iteration re-stages.
-      barrier_vmcnt<kStores>();
+      // The next stage has landed in LDS (every wave's pieces) and every wave
+      // is done reading this one, which the next iteration re-stages.  Its
+      // DMA was issued before this stage's (ge - gb) x kStores output stores.
+      if (ge - gb == kH3GroupsPerStage) barrier_vmcnt<kH3GroupsPerStage * kStores>();
+      else barrier_vmcnt<kStores>();
     }
   }
 }
@@ -386,7 +404,7 @@ __global__ __launch_bounds__(256, MANO_SPAN_H3_BLOCKS_PER_CU) void skin_span_h3_
                   int(threadIdx.x & 63));
 }
 
-constexpr int kBlendSkinH3BlocksPerCU = 8 / kH3Waves;  // 64 KB LDS ring per block, 2 waves per SIMD
+constexpr int kBlendSkinH3BlocksPerCU = 8 / kH3Waves;  // 2 waves per SIMD; 64 KB x kH3GroupsPerStage of LDS per block
 constexpr int kSkinH3BlocksPerCU = MANO_SPAN_H3_BLOCKS_PER_CU;
 constexpr int64_t kMinUnitsPerWorkerH3 = 8;
 
