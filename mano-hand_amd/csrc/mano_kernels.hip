@@ -173,8 +173,15 @@ __global__ __launch_bounds__(256) void articulate_kernel(
     float* __restrict__ features, float* __restrict__ transforms, float* __restrict__ joints,
     float* __restrict__ rest_joints, float* __restrict__ rot_mats) {
   __shared__ f32x4 xs4[16 * kXStride / 4];
+  // The folded joint regressor (J = Jt + Js . beta, 528 floats), staged once
+  // per block: each lane reads its joint's 33 values from LDS, not HBM/L2.
+  __shared__ float jt_s[kJoints * 3];
+  __shared__ float js_s[kJoints * 3 * kShape];
   float* xs = reinterpret_cast<float*>(xs4);
   const int tid = threadIdx.x;
+  for (int i = tid; i < kJoints * 3 * kShape; i += 256) js_s[i] = joint_shape[i];
+  if (tid < kJoints * 3) jt_s[tid] = joint_template[tid];
+  __syncthreads();
   const int j = tid & (kJoints - 1);
   const int hl = tid >> 4;
   const int64_t h0 = int64_t(blockIdx.x) * 16;
@@ -188,8 +195,7 @@ __global__ __launch_bounds__(256) void articulate_kernel(
   const int par = parents[j];
   const int src = ((tid & 63) & ~(kJoints - 1)) + (par < 0 ? 0 : par);
   float rm[9], J[3], t[3], Aj[12];
-  articulate_joint(p[0], p[1], p[2], beta, j, src, depth[j], max_depth, joint_template, joint_shape,
-                   rm, J, t, Aj);
+  articulate_joint(p[0], p[1], p[2], beta, j, src, depth[j], max_depth, jt_s, js_s, rm, J, t, Aj);
   if (valid) {
     f32x4* A = reinterpret_cast<f32x4*>(transforms + h * kTransformFloats + j * 12);
     A[0] = f32x4{Aj[0], Aj[1], Aj[2], Aj[3]};
