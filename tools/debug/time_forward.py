@@ -26,8 +26,16 @@ for prec in ("fp32", "f16x3"):
         a.record(); m.stage_blend_skin(B, v); b.record()
     torch.cuda.synchronize()
     ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    for _ in range(300):
+        m.stage_articulate(betas, pose)
+    ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(200)]
+    for a, b in ev2:
+        a.record(); m.stage_articulate(betas, pose); b.record()
+    torch.cuda.synchronize()
+    ms_art = float(np.mean([a.elapsed_time(b) for a, b in ev2]))
     if ref is None:
         ref = v.clone()
     err = (v - ref).abs().max().item()
-    print(f"{os.path.basename(_abi.LIB_PATH):24s} {prec:6s} blend_skin {ms:.4f} ms  vs fp32 max {err:.2e}", flush=True)
+    print(f"{os.path.basename(_abi.LIB_PATH):24s} {prec:6s} blend_skin {ms:.4f} ms  articulate {ms_art:.4f} ms  "
+          f"vs fp32 max {err:.2e}", flush=True)
     m.close()
