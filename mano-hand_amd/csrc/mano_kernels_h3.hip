@@ -195,10 +195,14 @@ __device__ __forceinline__ void unit_range_h3(int64_t units, int64_t worker, int
 #define MANO_H3_WAVES 8
 #endif
 constexpr int kH3Waves = MANO_H3_WAVES;  // waves (16-hand tiles) per blend_skin_h3 block
-#ifndef MANO_H3_GROUPS_PER_STAGE
-#define MANO_H3_GROUPS_PER_STAGE 1
+#ifndef MANO_H3_TPW
+#define MANO_H3_TPW 1
 #endif
-constexpr int kH3GroupsPerStage = MANO_H3_GROUPS_PER_STAGE;  // vertex groups per barrier
+constexpr int kH3TPW = MANO_H3_TPW;  // 16-hand tiles per wave (each B piece read feeds them all)
+#ifndef MANO_H3_BLOCKS
+#define MANO_H3_BLOCKS 1
+#endif
+constexpr int kH3BlocksPerCU = MANO_H3_BLOCKS;
 
 // One group's 32 fragment pieces (32 KB), global -> LDS, 32 / kH3Waves per wave.
 __device__ __forceinline__ void stage_group_h3(const uint16_t* __restrict__ basis_h3, int grp,
@@ -215,121 +219,133 @@ __device__ __forceinline__ void stage_group_h3(const uint16_t* __restrict__ basi
   asm volatile("" ::: "memory");
 }
 
-// Fused blend GEMM + LBS, f16x3.  A block (4 waves, one 16-hand tile each)
-// owns a contiguous range of (quad of 4 hand tiles, vertex group) units; the
-// group's basis + weight pieces are LDS-DMA-staged once per block, one group
-// ahead (ring of 2 x 32 KB).  hipcc does not order LDS-DMA against the
-// barrier, so each group ends with an explicit vmcnt wait: the next group's
-// DMA was issued before this group's kStores output stores, so vmcnt(kStores)
-// covers it without waiting for the stores themselves.  Stores are branch-free
-// (rows past the batch end rewrite the last hand's identical values), so their
-// count is exact.
+// Fused blend GEMM + LBS, f16x3.  A block (kH3Waves waves, kH3TPW 16-hand
+// tiles each) owns a contiguous range of (block tile set, vertex group)
+// units; the group's basis + weight pieces are LDS-DMA-staged once per block,
+// one group ahead (ring of 2 x 32 KB), and every B piece a wave reads feeds its
+// kH3TPW tiles.  Each group ends with an explicit vmcnt wait: the next
+// group's DMA was issued before this group's kStores output stores, so
+// vmcnt(kStores) covers it without waiting for the stores themselves.  Stores
+// are branch-free (rows past the batch end rewrite the last hand's identical
+// values), so their count is exact.
 template <bool kTrans, bool kVposed>
-__global__ __launch_bounds__(64 * kH3Waves, 8 / kH3Waves) void blend_skin_h3_kernel(
+__global__ __launch_bounds__(64 * kH3Waves, kH3BlocksPerCU) void blend_skin_h3_kernel(
     const float* __restrict__ features, const float* __restrict__ transforms,
     const uint16_t* __restrict__ basis_h3, const float* __restrict__ trans,
     float* __restrict__ verts, float* __restrict__ vposed, int64_t n, int n_verts, int n_groups,
     float p_unscale, float t_unscale) {
-  constexpr int kSlot = kH3GroupPieces * 64;  // f16x8 per slot (32 KB)
-  constexpr int kStores = kVposed ? 8 : 4;    // global_store_dwordx3 per group
-  __shared__ f16x8 ring[2 * kH3GroupsPerStage * kSlot];
+  constexpr int kSlot = kH3GroupPieces * 64;                // f16x8 per slot (32 KB)
+  constexpr int kStores = (kVposed ? 8 : 4) * kH3TPW;       // global_store_dwordx3 per group
+  constexpr int kTiles = kH3Waves * kH3TPW;                 // hand tiles per block unit
+  __shared__ f16x8 ring[2 * kSlot];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int vstride = 3 * n_verts;
   const int64_t nt16 = (n + 15) / 16;
-  const int64_t n_quads = (nt16 + kH3Waves - 1) / kH3Waves;
+  const int64_t n_sets = (nt16 + kTiles - 1) / kTiles;
   int64_t u, u_end;
-  unit_range_h3(n_quads * n_groups, blockIdx.x, gridDim.x, u, u_end);
+  unit_range_h3(n_sets * n_groups, blockIdx.x, gridDim.x, u, u_end);
 
   while (u < u_end) {
-    const int64_t quad = u / n_groups;
-    const int g0 = int(u - quad * n_groups);
+    const int64_t set = u / n_groups;
+    const int g0 = int(u - set * n_groups);
     const int g1 = int(n_groups - g0 < u_end - u ? n_groups : g0 + (u_end - u));
     u += g1 - g0;
-    // A wave past the batch end recomputes the last tile (identical values).
-    const int64_t h0 = min(quad * kH3Waves + wave, nt16 - 1) * 16;
-    const int rmax = int(n - 1 - h0 < 15 ? n - 1 - h0 : 15);  // last row of the tile in the batch
 
     int lane = threadIdx.x & 63;
     asm volatile("" : "+v"(lane));  // keep lane-derived addresses inside the range loop
     const int q = lane >> 4;
     const int col = lane & 15;
 
-    // Stages of kH3GroupsPerStage groups, double-buffered: stage st holds
-    // groups [gb, ge) in slots st * kH3GroupsPerStage + i.
-    auto stage_groups = [&](int gb, int ge, int st) {
-      for (int i = 0; i < kH3GroupsPerStage; ++i)
-        if (gb + i < ge) stage_group_h3(basis_h3, gb + i, ring + (st * kH3GroupsPerStage + i) * kSlot, wave, lane);
-    };
-    stage_groups(g0, min(g0 + kH3GroupsPerStage, g1), 0);
-    f16x8 xh[kH3Steps], xl[kH3Steps], F[12];
-    load_x_h3(features + (h0 + min(col, rmax)) * kXStride, q, xh, xl);
-    load_frames_h3(transforms, h0, n, lane, F);
-    operand_fence(xh);
-    operand_fence(xl);
-    operand_fence(F);
-    float tr[4][3] = {};
-    unsigned roff[4];  // this lane's D rows (hands 4q + r) in the tile, clamped to the batch
+    stage_group_h3(basis_h3, g0, ring, wave, lane);
+    f16x8 xh[kH3TPW][kH3Steps], xl[kH3TPW][kH3Steps], F[kH3TPW][12];
+    float tr[kH3TPW][4][3] = {};
+    unsigned roff[kH3TPW][4];  // D rows (hands 4q + r) of each tile, clamped to the batch
+    float* vtile[kH3TPW];
+    float* ptile[kH3TPW];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int hr = min(4 * q + r, rmax);
-      roff[r] = unsigned(hr * vstride + 3 * col);
-      if constexpr (kTrans) {
+    for (int t = 0; t < kH3TPW; ++t) {
+      // A tile past the batch end recomputes the last tile (identical values).
+      const int64_t h0 = min(set * kTiles + wave * kH3TPW + t, nt16 - 1) * 16;
+      const int rmax = int(n - 1 - h0 < 15 ? n - 1 - h0 : 15);  // last row of the tile in the batch
+      load_x_h3(features + (h0 + min(col, rmax)) * kXStride, q, xh[t], xl[t]);
+      load_frames_h3(transforms, h0, n, lane, F[t]);
+      operand_fence(xh[t]);
+      operand_fence(xl[t]);
+      operand_fence(F[t]);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) tr[r][c] = trans[(h0 + hr) * 3 + c];
+      for (int r = 0; r < 4; ++r) {
+        const int hr = min(4 * q + r, rmax);
+        roff[t][r] = unsigned(hr * vstride + 3 * col);
+        if constexpr (kTrans) {
+#pragma unroll
+          for (int c = 0; c < 3; ++c) tr[t][r][c] = trans[(h0 + hr) * 3 + c];
+        }
       }
+      vtile[t] = verts + h0 * int64_t(vstride);
+      ptile[t] = kVposed ? vposed + h0 * int64_t(vstride) : nullptr;
     }
-    float* vtile = verts + h0 * int64_t(vstride);
-    float* ptile = kVposed ? vposed + h0 * int64_t(vstride) : nullptr;
     // The first group's pieces and every prologue load have landed.
     barrier_vmcnt<0>();
 
-    for (int gb = g0, st = 0; gb < g1; gb += kH3GroupsPerStage, st ^= 1) {
-      const int ge = min(gb + kH3GroupsPerStage, g1);
-      if (ge < g1) stage_groups(ge, min(ge + kH3GroupsPerStage, g1), st ^ 1);
+    for (int grp = g0, slot = 0; grp < g1; ++grp, slot ^= 1) {
+      if (grp + 1 < g1) stage_group_h3(basis_h3, grp + 1, ring + (slot ^ 1) * kSlot, wave, lane);
+      const f16x8* L = ring + slot * kSlot + lane;
+      // The coordinates' (and tiles') chains interleaved (independent
+      // accumulators), each summing hi.lo, lo.hi, then hi.hi over the 5 K-steps.
+      f32x4 p[kH3TPW][3];
 #pragma unroll
-      for (int i = 0; i < kH3GroupsPerStage; ++i) {
-        const int grp = gb + i;
-        if (grp >= ge) break;
-        const f16x8* L = ring + (st * kH3GroupsPerStage + i) * kSlot + lane;
-        // The three coordinates' chains interleaved (independent accumulators),
-        // each summing hi.lo, lo.hi, then hi.hi over the 5 K-steps.
-        f32x4 p[3];
+      for (int c = 0; c < 3; ++c) {
+        const f16x8 b = L[((2 * c + 1) * kH3Steps) * 64];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) mfma_init(p[c], xh[0], L[((2 * c + 1) * kH3Steps) * 64]);
+        for (int t = 0; t < kH3TPW; ++t) mfma_init(p[t][c], xh[t][0], b);
+      }
 #pragma unroll
-        for (int s = 1; s < kH3Steps; ++s)
+      for (int s = 1; s < kH3Steps; ++s)
 #pragma unroll
-          for (int c = 0; c < 3; ++c) mfma_acc(p[c], xh[s], L[((2 * c + 1) * kH3Steps + s) * 64]);
+        for (int c = 0; c < 3; ++c) {
+          const f16x8 b = L[((2 * c + 1) * kH3Steps + s) * 64];
 #pragma unroll
-        for (int s = 0; s < kH3Steps; ++s)
+          for (int t = 0; t < kH3TPW; ++t) mfma_acc(p[t][c], xh[t][s], b);
+        }
 #pragma unroll
-          for (int c = 0; c < 3; ++c) mfma_acc(p[c], xl[s], L[((2 * c) * kH3Steps + s) * 64]);
+      for (int s = 0; s < kH3Steps; ++s)
 #pragma unroll
-        for (int s = 0; s < kH3Steps; ++s)
+        for (int c = 0; c < 3; ++c) {
+          const f16x8 b = L[((2 * c) * kH3Steps + s) * 64];
 #pragma unroll
-          for (int c = 0; c < 3; ++c) mfma_acc(p[c], xh[s], L[((2 * c) * kH3Steps + s) * 64]);
-        mfma_fence(p);
+          for (int t = 0; t < kH3TPW; ++t) mfma_acc(p[t][c], xl[t][s], b);
+        }
+#pragma unroll
+      for (int s = 0; s < kH3Steps; ++s)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const f16x8 b = L[((2 * c) * kH3Steps + s) * 64];
+#pragma unroll
+          for (int t = 0; t < kH3TPW; ++t) mfma_acc(p[t][c], xh[t][s], b);
+        }
+      const int voff = 3 * min(grp * 16, n_verts - 16);
+      const f16x8 w1 = L[kH3WPiece * 64];
+      const f16x8 w2 = L[(kH3WPiece + 1) * 64];
+#pragma unroll
+      for (int t = 0; t < kH3TPW; ++t) {
+        mfma_fence(p[t]);
 #pragma unroll
         for (int c = 0; c < 3; ++c)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) p[c][r] = no_pack(p[c][r] * p_unscale);
-        const int voff = 3 * min(grp * 16, n_verts - 16);
-        const f16x8 w1 = L[kH3WPiece * 64];
-        const f16x8 w2 = L[(kH3WPiece + 1) * 64];
+          for (int r = 0; r < 4; ++r) p[t][c][r] = no_pack(p[t][c][r] * p_unscale);
         f32x4 out[3];
-        lbs_h3(F, w1, w2, p, t_unscale, tr, out);
+        lbs_h3(F[t], w1, w2, p[t], t_unscale, tr[t], out);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          *reinterpret_cast<f32x3*>(vtile + (roff[r] + voff)) = f32x3{out[0][r], out[1][r], out[2][r]};
+          *reinterpret_cast<f32x3*>(vtile[t] + (roff[t][r] + voff)) = f32x3{out[0][r], out[1][r], out[2][r]};
           if constexpr (kVposed)
-            *reinterpret_cast<f32x3*>(ptile + (roff[r] + voff)) = f32x3{p[0][r], p[1][r], p[2][r]};
+            *reinterpret_cast<f32x3*>(ptile[t] + (roff[t][r] + voff)) =
+                f32x3{p[t][0][r], p[t][1][r], p[t][2][r]};
         }
       }
-      // The next stage has landed in LDS (every wave's pieces) and every wave
-      // is done reading this one, which the next iteration re-stages.  Its
-      // DMA was issued before this stage's (ge - gb) x kStores output stores.
-      if (ge - gb == kH3GroupsPerStage) barrier_vmcnt<kH3GroupsPerStage * kStores>();
-      else barrier_vmcnt<kStores>();
+      // Group grp + 1 has landed in LDS (every wave's pieces) and every wave
+      // is done reading this slot, which the next iteration re-stages.
+      barrier_vmcnt<kStores>();
     }
   }
 }
@@ -404,7 +420,7 @@ __global__ __launch_bounds__(256, MANO_SPAN_H3_BLOCKS_PER_CU) void skin_span_h3_
                   int(threadIdx.x & 63));
 }
 
-constexpr int kBlendSkinH3BlocksPerCU = 8 / kH3Waves;  // 2 waves per SIMD; 64 KB x kH3GroupsPerStage of LDS per block
+constexpr int kBlendSkinH3BlocksPerCU = kH3BlocksPerCU;  // 64 KB of LDS per block
 constexpr int kSkinH3BlocksPerCU = MANO_SPAN_H3_BLOCKS_PER_CU;
 constexpr int64_t kMinUnitsPerWorkerH3 = 8;
 
@@ -425,7 +441,7 @@ dim3 persistent_grid_h3(Kernel kernel, const DeviceModel& m, int64_t units, int 
 hipError_t launch_blend_skin_h3(const DeviceModel& m, int64_t n, const float* features,
                                 const float* transforms, const float* trans, float* verts,
                                 float* vposed, hipStream_t stream) {
-  const int64_t units = ((n + 15) / 16 + kH3Waves - 1) / kH3Waves * m.n_groups16;
+  const int64_t units = ((n + 15) / 16 + kH3Waves * kH3TPW - 1) / (kH3Waves * kH3TPW) * m.n_groups16;
   auto launch = [&](auto kernel) {
     hipLaunchKernelGGL(kernel, persistent_grid_h3(kernel, m, units, 1, kBlendSkinH3BlocksPerCU, 64 * kH3Waves),
                        dim3(64 * kH3Waves), 0, stream, features, transforms, m.basis_h3, trans, verts, vposed,
