@@ -602,6 +602,7 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
 template <bool kTrans>
 struct SpanLbs16 {
   using W = f32x4;
+  static constexpr bool kInPlace = true;
   struct Tile {
     float F[12][4];
     float tr[4][3];
@@ -646,7 +647,7 @@ __global__ __launch_bounds__(256, MANO_SPAN_BLOCKS_PER_CU) void skin_span_kernel
   __shared__ f32x4 stage[4 * span::kStageFloats / 4];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   SpanLbs16<kTrans> lbs{transforms, wfrag16, trans, {}};
-  span::run_units<true>(lbs, vposed, verts, n, n_verts, n_groups, span::xcd_worker(wave),
+  span::run_units<true, 3, MANO_SPAN_CHUNK>(lbs, vposed, verts, n, n_verts, n_groups, span::xcd_worker(wave),
                   int64_t(gridDim.x) * 4, reinterpret_cast<float*>(stage) + wave * span::kStageFloats,
                   int(threadIdx.x & 63));
 }

@@ -356,6 +356,7 @@ __global__ __launch_bounds__(64 * kH3Waves, kH3BlocksPerCU) void blend_skin_h3_k
 // blend_skin_h3's LBS bit for bit.
 template <bool kTrans>
 struct SpanLbsH3 {
+  static constexpr bool kInPlace = false;
   struct W {
     f16x8 w1, w2;
   };
@@ -415,7 +416,7 @@ __global__ __launch_bounds__(256, MANO_SPAN_H3_BLOCKS_PER_CU) void skin_span_h3_
   __shared__ f32x4 stage[4 * span::kStageFloats / 4];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   SpanLbsH3<kTrans> lbs{transforms, basis_h3, trans, t_unscale, int(threadIdx.x & 63), {}, {}};
-  span::run_units<false>(lbs, vposed, verts, n, n_verts, n_groups, int64_t(blockIdx.x) * 4 + wave,
+  span::run_units<false, 0, 1>(lbs, vposed, verts, n, n_verts, n_groups, int64_t(blockIdx.x) * 4 + wave,
                   int64_t(gridDim.x) * 4, reinterpret_cast<float*>(stage) + wave * span::kStageFloats,
                   int(threadIdx.x & 63));
 }

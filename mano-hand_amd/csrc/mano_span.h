@@ -32,6 +32,9 @@ typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
 #ifndef MANO_SPAN_VERTS
 #define MANO_SPAN_VERTS 64
 #endif
+#ifndef MANO_SPAN_CHUNK
+#define MANO_SPAN_CHUNK 1             // skin_span: consecutive units per grid-stride step
+#endif
 #ifndef MANO_SPAN_BLOCKS_PER_CU
 #define MANO_SPAN_BLOCKS_PER_CU 2     // skin_span: <= 256 VGPRs, 2 waves per SIMD
 #endif
@@ -144,13 +147,17 @@ __device__ __forceinline__ int64_t xcd_worker(int wave) {
 // rows are prefetched (vmcnt retires in issue order: waiting for a load
 // issued after the prefetch would wait for the prefetch too; and the f16x3
 // operands are split in registers, which needs them landed), their latency
-// covered by the other wave on the SIMD.  Lbs supplies:
+// covered by the other wave on the SIMD.  kPrio != 0 raises the wave's issue
+// priority while it issues a unit's row loads and stores, so the HBM stream is
+// not held behind the sibling wave's MFMAs (fp32 skin_span: 0.305 -> 0.297 ms
+// at kPrio 3; the f16x3 kernel, one wave per SIMD, gains nothing).  Lbs supplies:
 //   typename Lbs::W, Lbs::Tile          one group's weights, one tile's operands
 //   W    load_w(int grp, int lane)
 //   void fetch_tile(int64_t h0, int64_t n, int n_valid, int lane, Tile&)
 //   void set_tile(const Tile&)           make them the current operands
+//   Tile cur; static constexpr bool kInPlace  fetch_tile may write cur directly
 //   void apply(const W&, const float (&p)[4][3], float (&o)[4][3])
-template <bool kStride, class Lbs>
+template <bool kStride, int kPrio, int kChunk, class Lbs>
 __device__ __forceinline__ void run_units(Lbs& lbs, const float* __restrict__ vposed,
                                           float* __restrict__ verts, int64_t n, int n_verts,
                                           int n_groups, int64_t worker, int64_t n_workers,
@@ -198,29 +205,42 @@ __device__ __forceinline__ void run_units(Lbs& lbs, const float* __restrict__ vp
   // kStride: units worker + k n_workers (operands fetched per unit);
   // otherwise the contiguous range [u_begin, u_end), tile-major (operands
   // fetched when the tile changes).
-  const int64_t u_begin = kStride ? worker : worker * units / n_workers;
+  // kStride with kChunk > 1: chunks of kChunk consecutive units in the
+  // grid-stride order (the spans of a chunk mostly share a tile, whose
+  // operands are then fetched once).
+  const int64_t u_begin = kStride ? worker * kChunk : worker * units / n_workers;
   const int64_t u_end = kStride ? units : (worker + 1) * units / n_workers;
-  const int64_t u_step = kStride ? n_workers : 1;
+  auto next_unit = [&](int64_t uu) -> int64_t {
+    if (!kStride || kChunk == 1) return uu + (kStride ? n_workers : 1);
+    return (uu + 1) % kChunk ? uu + 1 : uu + 1 + (n_workers - 1) * kChunk;
+  };
   int64_t cur_tile = -1;
   fetch_rows(u_begin);
-  for (int64_t uu = u_begin; uu < u_end; uu += u_step) {
+  for (int64_t uu = u_begin; uu < u_end; uu = next_unit(uu)) {
     const int64_t tile = uu / spans;
     const int s = int(uu - tile * spans);
     const int64_t h0 = tile * 16;
     const int n_valid = rows_of(tile);
     const bool full = s < n_full;
-    const bool new_tile = kStride || tile != cur_tile;
+    const bool new_tile = (kStride && kChunk == 1) || tile != cur_tile;
     cur_tile = tile;
+    // Lbs::kInPlace: the operands load straight into the current ones (the
+    // previous unit's are dead here), so no second copy is live.
     typename Lbs::Tile tops;
-    if (new_tile) lbs.fetch_tile(h0, n, n_valid, lane, tops);
+    if (new_tile) {
+      if constexpr (Lbs::kInPlace) lbs.fetch_tile(h0, n, n_valid, lane, lbs.cur);
+      else lbs.fetch_tile(h0, n, n_valid, lane, tops);
+    }
     typename Lbs::W w[kGroups];
 #pragma unroll
     for (int g = 0; g < kGroups; ++g)
       if (full || g < n_tail) w[g] = lbs.load_w(kGroups * (full ? s : n_full) + g, lane);
     if (full) {
       put_rows(stage, lane, buf);
-      if (new_tile) lbs.set_tile(tops);
-      if (uu + u_step < u_end) fetch_rows(uu + u_step);
+      if (!Lbs::kInPlace && new_tile) lbs.set_tile(tops);
+      if constexpr (kPrio != 0) __builtin_amdgcn_s_setprio(kPrio);
+      if (next_unit(uu) < u_end) fetch_rows(next_unit(uu));
+      if constexpr (kPrio != 0) __builtin_amdgcn_s_setprio(0);
       wave_sync();
 #pragma unroll
       for (int g = 0; g < kGroups; ++g) {
@@ -231,7 +251,9 @@ __device__ __forceinline__ void run_units(Lbs& lbs, const float* __restrict__ vp
         __builtin_amdgcn_sched_barrier(0);  // one group's LBS temporaries live at a time
       }
       wave_sync();
+      if constexpr (kPrio != 0) __builtin_amdgcn_s_setprio(kPrio);
       store_rows(stage, verts + h0 * vstride, vstride, kVerts * s, n_valid, lane);
+      if constexpr (kPrio != 0) __builtin_amdgcn_s_setprio(0);
       wave_sync();
     } else {
       float p[kGroups][4][3];
@@ -241,8 +263,8 @@ __device__ __forceinline__ void run_units(Lbs& lbs, const float* __restrict__ vp
         for (int r = 0; r < 4; ++r)
 #pragma unroll
           for (int c = 0; c < 3; ++c) p[g][r][c] = buf[(12 * g + 3 * r + c) >> 2][(12 * g + 3 * r + c) & 3];
-      if (new_tile) lbs.set_tile(tops);
-      if (uu + u_step < u_end) fetch_rows(uu + u_step);
+      if (!Lbs::kInPlace && new_tile) lbs.set_tile(tops);
+      if (next_unit(uu) < u_end) fetch_rows(next_unit(uu));
       float* dst = verts + h0 * vstride;
 #pragma unroll
       for (int g = 0; g < kGroups; ++g) {
