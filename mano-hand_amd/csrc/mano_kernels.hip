@@ -457,6 +457,22 @@ __device__ __forceinline__ void barrier_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
+// Wave issue priority around a short issue section (s_setprio; 0 = unchanged).
+template <int P>
+__device__ __forceinline__ void prio_up() {
+  if constexpr (P != 0) __builtin_amdgcn_s_setprio(P);
+}
+template <int P>
+__device__ __forceinline__ void prio_down() {
+  if constexpr (P != 0) __builtin_amdgcn_s_setprio(0);
+}
+#ifndef MANO_BS_DMA_PRIO
+#define MANO_BS_DMA_PRIO 1    // blend_skin16: priority while issuing the basis LDS-DMA (0.512 -> 0.506 ms)
+#endif
+#ifndef MANO_BS_STORE_PRIO
+#define MANO_BS_STORE_PRIO 0  // blend_skin16: priority while issuing the point stores
+#endif
+
 // Fused blend GEMM + LBS.  A block owns a contiguous range of (quad of 4
 // hand tiles, vertex group) units; at each quad its waves load their A
 // fragments (the X rows written by articulate_kernel) and LBS fragments (the
@@ -480,6 +496,7 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
   // t + 1's DMA -- tile t + 2's DMA (at least 2 pieces per wave) and, after a
   // group's first tile, the previous group's stores.
   constexpr int kPieces = kGroups16 / 4;     // LDS-DMA pieces per wave and tile, at least
+  constexpr int kDmaPrio = MANO_BS_DMA_PRIO, kStorePrio = MANO_BS_STORE_PRIO;
   __shared__ f32x4 lds[3 * kRingF4];
   __shared__ float trs[4][16 * 3];  // the wave's 16 translations, read back at the stores
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -550,19 +567,27 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
       const bool more = grp + 1 < g1;
       f32x4 p[3];
       // Tile 3 grp + q in slot q; tile 3 grp + q + 2 goes to slot (q + 2) % 3.
+      prio_up<kDmaPrio>();
       stage_basis_tile16(basis16, 3 * grp + 2, lds + 2 * kRingF4, wave, lane);
+      prio_down<kDmaPrio>();
       const f32x4 wf = lds[kGroups16 * 64 + lane];  // read before slot 0 is re-staged
       p[0] = mfma16_tile(a, lds, lane);
       if (grp == g0) barrier_vmcnt<kPieces>();
       else barrier_vmcnt<kPieces + kStores>();
       if (more) {
+        prio_up<kDmaPrio>();
         stage_basis_tile16(basis16, 3 * grp + 3, lds, wave, lane);
         stage_w(grp + 1, lds);
+        prio_down<kDmaPrio>();
       }
       p[1] = mfma16_tile(a, lds + kRingF4, lane);
       if (more) barrier_vmcnt<kPieces>();
       else barrier_vmcnt<0>();
-      if (more) stage_basis_tile16(basis16, 3 * grp + 4, lds + kRingF4, wave, lane);
+      if (more) {
+        prio_up<kDmaPrio>();
+        stage_basis_tile16(basis16, 3 * grp + 4, lds + kRingF4, wave, lane);
+        prio_down<kDmaPrio>();
+      }
       p[2] = mfma16_tile(a, lds + 2 * kRingF4, lane);
       if (more) barrier_vmcnt<kPieces>();
       else barrier_vmcnt<0>();
@@ -571,6 +596,7 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
       const int voff = 3 * (vb + col);
       f32x4 out[3];
       lbs_apply16(F, wf, p, out);
+      prio_up<kStorePrio>();
       // One 12-B point store per row; rows past the batch end rewrite the
       // last hand's identical values.
 #pragma unroll
@@ -586,6 +612,7 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
         if constexpr (kVposed)
           *reinterpret_cast<f32x3*>(ptile + unsigned(hr * vstride32 + voff)) = f32x3{p[0][r], p[1][r], p[2][r]};
       }
+      prio_down<kStorePrio>();
     }
   }
 }

@@ -175,6 +175,10 @@ __device__ __forceinline__ void lbs_h3(const f16x8 (&F)[12], const f16x8& w1, co
     }
 }
 
+#ifndef MANO_H3_DMA_PRIO
+#define MANO_H3_DMA_PRIO 0  // blend_skin_h3: wave priority while issuing the next group's LDS-DMA (1 and 3 measured: within noise)
+#endif
+
 // Workgroup barrier after s_waitcnt vmcnt(N) lgkmcnt(0): every vector-memory
 // op of this wave but the N youngest has completed (loads, stores and LDS-DMA
 // count together, in issue order) and every LDS access.  __syncthreads() would
@@ -288,7 +292,11 @@ __global__ __launch_bounds__(64 * kH3Waves, kH3BlocksPerCU) void blend_skin_h3_k
     barrier_vmcnt<0>();
 
     for (int grp = g0, slot = 0; grp < g1; ++grp, slot ^= 1) {
-      if (grp + 1 < g1) stage_group_h3(basis_h3, grp + 1, ring + (slot ^ 1) * kSlot, wave, lane);
+      if (grp + 1 < g1) {
+        if constexpr (MANO_H3_DMA_PRIO != 0) __builtin_amdgcn_s_setprio(MANO_H3_DMA_PRIO);
+        stage_group_h3(basis_h3, grp + 1, ring + (slot ^ 1) * kSlot, wave, lane);
+        if constexpr (MANO_H3_DMA_PRIO != 0) __builtin_amdgcn_s_setprio(0);
+      }
       const f16x8* L = ring + slot * kSlot + lane;
       // The coordinates' (and tiles') chains interleaved (independent
       // accumulators), each summing hi.lo, lo.hi, then hi.hi over the 5 K-steps.
