@@ -416,6 +416,12 @@ struct SpanLbsH3 {
   }
 };
 
+#ifndef MANO_SPAN_H3_STRIDE
+#define MANO_SPAN_H3_STRIDE false  // skin_span_h3: tile-major per-wave ranges (split operands built once per tile)
+#endif
+#ifndef MANO_SPAN_H3_PRIO
+#define MANO_SPAN_H3_PRIO 0
+#endif
 template <bool kTrans>
 __global__ __launch_bounds__(256, MANO_SPAN_H3_BLOCKS_PER_CU) void skin_span_h3_kernel(
     const float* __restrict__ transforms, const uint16_t* __restrict__ basis_h3,
@@ -424,7 +430,9 @@ __global__ __launch_bounds__(256, MANO_SPAN_H3_BLOCKS_PER_CU) void skin_span_h3_
   __shared__ f32x4 stage[4 * span::kStageFloats / 4];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   SpanLbsH3<kTrans> lbs{transforms, basis_h3, trans, t_unscale, int(threadIdx.x & 63), {}, {}};
-  span::run_units<false, 0, 1>(lbs, vposed, verts, n, n_verts, n_groups, int64_t(blockIdx.x) * 4 + wave,
+  span::run_units<MANO_SPAN_H3_STRIDE, MANO_SPAN_H3_PRIO, 1>(
+      lbs, vposed, verts, n, n_verts, n_groups,
+      MANO_SPAN_H3_STRIDE ? span::xcd_worker(wave) : int64_t(blockIdx.x) * 4 + wave,
                   int64_t(gridDim.x) * 4, reinterpret_cast<float*>(stage) + wave * span::kStageFloats,
                   int(threadIdx.x & 63));
 }
