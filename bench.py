@@ -119,7 +119,7 @@ def main():
     from mano_amd import ManoHip, load_dump, synthetic_params
     from mano_amd.distributed import gather_to_root
     params = load_dump(args.model) if args.model else synthetic_params(0)
-    model = ManoHip(params, device=local, precision=args.precision)
+    model = ManoHip(params, device=local_dev, precision=args.precision)
 
     B = args.batch
     g = torch.Generator(device=dev).manual_seed(1001 + rank)
