@@ -1,22 +1,43 @@
 """Throughput benchmark of the MI355X MANO forward pass (driver contract).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--gather]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload C2|C3|C4|C5]
 
 One step = one forward pass (mano_forward: articulate, then the fused blend
-GEMM + LBS kernel) over B hands per GPU
-(BASELINE.json configs[1]: 65,536 hands, fp32 full pose, random betas), inputs
-resident in HBM before the timed region.  N > 1 runs one process per GPU
-(torch.distributed.run); shards are independent (no collective on the hot
-path), `--gather` adds the RCCL gather of verts + joints to GPU 0 (config C4).
+GEMM + LBS kernel) over the workload's hands per GPU, inputs resident in HBM
+before the timed region.  Workloads (BASELINE.json configs; per-GPU shard
+fixed as N grows, so `scaling` is "weak"):
+
+  C2  65,536 hands per GPU, full pose + per-hand betas, verts + joints (default:
+      BASELINE.json configs[1], the metric's config)
+  C3  2,097,152 hands per GPU (16M over 8 GPUs), per-shard outputs
+  C4  524,288 hands per GPU (4M over 8 GPUs) + gather of verts + joints to GPU 0
+      (RCCL, C-ABI mano_gather) inside every timed step
+  C5  1,048,576 hands per GPU, per-hand betas + global rotation + translation,
+      verts + joints
+
+`--gpus N` with no WORLD_SIZE in the environment launches N ranks itself
+(`python -m torch.distributed.run`, one process per GPU, started before this
+process touches a GPU); under torchrun each rank reads RANK / LOCAL_RANK /
+WORLD_SIZE.  Hand inputs come from the counter-based generator keyed by
+(seed, global hand index), so rank r's shard is exactly hands r*B..(r+1)*B-1
+of the same global batch at any N.  Shards are independent (no collective on
+the hot path).
+
+Before the untimed warmup the bench runs the step for `--ramp-seconds`
+(reported as `ramp`): the chip needs ~50 back-to-back launches to reach its
+steady clock (profiles/r01_kernel_trace_warmup.txt), so a short `--warmup`
+does not leave the timed steps on the ramp.
 
 Rank 0 prints ONE JSON line with the whole-node hands/s, the roofline of the
 dominant kernel (per-kernel durations from HIP events recorded on the launch
 stream inside the timed steps) and, at N = 1, the CPU baseline: the float64
-per-hand restatement of mano_np.py (oracle/, "port") timed on this host.
+restatement of mano_np.py (oracle/, "port") timed on this host's cores.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -25,14 +46,11 @@ sys.path.insert(0, os.path.join(REPO, "mano-hand_amd"))
 sys.path.insert(0, REPO)
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
 
-# Algorithmic work per hand (DESIGN.md "Rooflines").
+# Algorithmic work per hand.
 V, NCOL, K = 778, 2334, 145
 BLEND_FLOP_PER_HAND = 2 * NCOL * K                 # 676,860
 SKIN_BYTES_PER_HAND = NCOL * 4 * 2 + 16 * 12 * 4   # v_posed in + verts out + transforms = 19,440
-SKIN_FLOP_PER_HAND = V * (16 * 12 * 2 + 9 * 2)     # blend 16 transforms + apply = 312,312
 LBS_T_FLOP_PER_HAND = V * 16 * 12 * 2              # the transform blend (on MFMA when fused) = 298,752
 FUSED_MFMA_FLOP_PER_HAND = BLEND_FLOP_PER_HAND + LBS_T_FLOP_PER_HAND  # 975,612
 FUSED_BYTES_PER_HAND = 160 * 4 + 16 * 12 * 4 + NCOL * 4     # X row + transforms in, verts out = 10,744
@@ -40,18 +58,29 @@ ARTICULATE_BYTES_PER_HAND = (10 + 48) * 4 + 16 * 12 * 4 + 16 * 3 * 4 + 160 * 4  
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, spec
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
+WORKLOADS = {
+    "C2": {"hands": 65536, "trans": False, "gather": False, "seed": 1002,
+           "desc": "C2: full-pose fp32 MANO forward, 65,536 hands per GPU, verts + joints"},
+    "C3": {"hands": 2097152, "trans": False, "gather": False, "seed": 1003,
+           "desc": "C3: 2,097,152 hands per GPU (16M over 8 GPUs), per-shard verts + joints"},
+    "C4": {"hands": 524288, "trans": False, "gather": True, "seed": 1004,
+           "desc": "C4: 524,288 hands per GPU (4M over 8 GPUs), RCCL gather of verts + joints to GPU 0"},
+    "C5": {"hands": 1048576, "trans": True, "gather": False, "seed": 1005,
+           "desc": "C5: 1,048,576 hands per GPU, per-hand betas + global rot + trans, verts + joints"},
+}
 
-def parse():
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # The chip takes ~50 back-to-back launches (~30 ms) to reach its steady
-    # clock: blend_skin16 ran 0.73 ms -> 0.52 ms across the first 50 launches of
-    # a cold box (profiles/r01_kernel_trace_warmup.txt), so the default warmup
-    # is well past that.
     ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=300)
-    ap.add_argument("--batch", type=int, default=65536, help="hands per GPU per step")
-    ap.add_argument("--gather", action="store_true", help="RCCL gather of verts+joints to GPU 0")
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--ramp-seconds", type=float, default=1.0,
+                    help="run the step this long before the warmup (clock ramp)")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="C2")
+    ap.add_argument("--batch", type=int, default=None, help="override hands per GPU per step")
+    ap.add_argument("--gather", action="store_true", default=None,
+                    help="gather verts+joints to GPU 0 each step (default: the workload's)")
     ap.add_argument("--path", choices=("forward", "api", "unfused"), default="forward",
                     help="forward: mano_forward's two kernels, each bracketed by events (default); "
                          "api: one mano_forward call per step; unfused: articulate + blend + skin")
@@ -59,51 +88,126 @@ def parse():
                     help="fp32: exact fp32 MFMA (default); f16x3: split-half MFMA "
                          "(include/mano_hip.h MANO_PRECISION_F16X3)")
     ap.add_argument("--model", default=None, help="dump_model.py pickle (default: synthetic seed 0)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample length")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample per form")
+    ap.add_argument("--cpu-procs", type=int, default=None,
+                    help="CPU-baseline processes (default: this box's CPU share, at most 16)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the untimed other-path kernel table")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
-                    help="process-group backend for N > 1 (gloo: CPU rehearsal, ranks may share a GPU)")
-    return ap.parse_args()
+                    help="process-group backend for N > 1 (gloo: rehearsal, ranks may share a GPU)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the N ranks, meet in a barrier, print the world and exit (no GPU)")
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(params, seconds):
-    """float64 per-hand restatement (oracle.forward_one), one core, bounded sample."""
-    from oracle import mano_oracle
-    p = {k: (np.asarray(v, dtype=np.float64) if k not in ("parents", "faces") else v)
-         for k, v in params.items()}
-    rng = np.random.default_rng(1000)
-    betas = rng.normal(0, 1, (256, 10))
-    pose = rng.normal(0, 0.5, (256, 16, 3))
-    n = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        mano_oracle.forward_one(p, betas[n % 256], pose[n % 256])
-        n += 1
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "hands/s", "cores": 1, "kind": "port",
-            "sample": f"{n} hands, one at a time, float64 numpy restatement of mano_np.py:81-115 "
-                      f"(oracle/mano_oracle.py forward_one), {dt:.1f} s on 1 host core"}
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_command(argv, n):
+    """torchrun command that re-runs this script as n ranks on one node."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+            os.path.abspath(__file__), *argv]
+
+
+def cpu_share():
+    """CPUs this process may use, at most 16 (the GPU box's share per GPU)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16))
+
+
+def cpu_baseline(procs, seconds):
+    """float64 restatement of mano_np.py:81-115 on `procs` host cores (oracle/cpu_baseline.py,
+    run as a child process so its workers share nothing with the GPU process)."""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "oracle", "cpu_baseline.py"),
+                        "--procs", str(procs), "--seconds", str(seconds)],
+                       capture_output=True, text=True, timeout=120 + 4 * seconds)
+    if r.returncode != 0:
+        return {"value": None, "error": r.stderr[-500:]}
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    ph, bt = res["per_hand"], res["batched"]
+    return {"value": ph["value"], "unit": "hands/s", "cores": procs, "kind": "port",
+            "sample": f"{ph['hands']} hands one at a time (oracle.forward_one: the reference's "
+                      f"batch-1 op sequence of mano_np.py:81-115 in float64 numpy) in {procs} "
+                      f"processes x {ph['seconds']:.1f} s, OMP_NUM_THREADS=1; "
+                      "beta ~ N(0,1), pose ~ N(0,0.5^2)",
+            "batched": {"value": bt["value"], "unit": "hands/s", "cores": procs,
+                        "sample": f"{bt['hands']} hands in 256-hand float64 einsum batches "
+                                  f"(oracle.forward) in {procs} processes x {bt['seconds']:.1f} s"}}
 
 
 def load_traffic(path, kernel, batch):
-    """HBM bytes per launch from a committed rocprofv3 --pmc summary, if it covers this batch."""
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary
+    (profiles/pmc_traffic.json, tools/pmc_traffic.py): the entry measured at this
+    batch, else the per-hand bytes of the largest measured batch x batch."""
     try:
         with open(path) as f:
             data = json.load(f)
-        ent = data["kernels"][kernel]
-        if int(data["batch"]) != batch:
-            return None
-        return float(ent["hbm_bytes_per_launch"])
+        ents = data["kernels"][kernel]
     except (OSError, KeyError, ValueError, TypeError):
-        return None
+        return None, None
+    if isinstance(ents, dict) and "batch" in data:  # round-1 single-batch form
+        ents = [dict(ents, batch=data["batch"])]
+    for e in ents:
+        if int(e["batch"]) == batch:
+            return float(e["hbm_bytes_per_launch"]), f"rocprofv3 --pmc at {batch} hands"
+    if not ents:
+        return None, None
+    e = max(ents, key=lambda x: int(x["batch"]))
+    return (float(e["hbm_bytes_per_launch"]) / int(e["batch"]) * batch,
+            f"rocprofv3 --pmc per-hand bytes at {e['batch']} hands x {batch}")
 
 
-def main():
-    args = parse()
+def launch_check(args):
+    """--launch-check: the N ranks meet over gloo and rank 0 prints the world (no GPU)."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+        t = torch.tensor([rank], dtype=torch.int64)
+        dist.all_reduce(t)
+        total = int(t.item())
+        dist.barrier()
+        dist.destroy_process_group()
+    else:
+        total = 0
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "rank_sum": total,
+                          "local_ranks_ok": total == world * (world - 1) // 2}), flush=True)
+
+
+def main(argv=None):
+    raw = sys.argv[1:] if argv is None else argv
+    args = parse(raw)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # Launch N ranks; this process never touches a GPU (it only waits).
+        sys.exit(subprocess.run(launch_command(raw, args.gpus)).returncode)
+    if args.launch_check:
+        return launch_check(args)
+
+    import torch
+    import torch.distributed as dist
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.gpus not in (1, world):
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+    wl = WORKLOADS[args.workload]
+    B = args.batch if args.batch else wl["hands"]
+    gather = wl["gather"] if args.gather is None else args.gather
+    with_trans = wl["trans"]
     # One process per GPU.  `--backend gloo` is a control-flow rehearsal mode
     # (several ranks may share one GPU); the real multi-GPU run uses RCCL.
     ndev = torch.cuda.device_count()
@@ -117,19 +221,25 @@ def main():
             dist.init_process_group("gloo")
 
     from mano_amd import ManoHip, load_dump, synthetic_params
-    from mano_amd.distributed import gather_to_root
+    from mano_amd.distributed import AbiGather, gather_to_root
     params = load_dump(args.model) if args.model else synthetic_params(0)
     model = ManoHip(params, device=local_dev, precision=args.precision)
 
-    B = args.batch
-    g = torch.Generator(device=dev).manual_seed(1001 + rank)
-    betas = torch.randn((B, 10), generator=g, device=dev)
-    pose = 0.5 * torch.randn((B, 16, 3), generator=g, device=dev)
+    # Shard r = global hands r*B .. (r+1)*B - 1 of one counter-based batch.
+    inp = model.synthetic_inputs(wl["seed"], rank * B, B, trans=with_trans)
+    betas, pose, trans = inp["betas"], inp["pose"], inp.get("trans")
     verts = torch.empty((B, V, 3), device=dev)
     joints = torch.empty((B, 16, 3), device=dev)
     stream = torch.cuda.current_stream(dev)
     out = {"verts": verts, "joints": joints}
     model.workspace(B)  # allocated before timing (covers every path)
+    gatherer, gv, gj = None, None, None
+    if gather and world > 1:
+        if args.backend == "nccl":
+            gatherer = AbiGather(local_dev)
+            if rank == 0:  # GPU 0's assembled buffers, allocated once
+                gv = torch.empty((B * world, V, 3), device=dev)
+                gj = torch.empty((B * world, 16, 3), device=dev)
 
     # Launch sequence of one step; `marks` get an event after each kernel.
     # "forward" issues exactly mano_forward's two launches (articulate, then
@@ -141,32 +251,43 @@ def main():
                 marks[i].record(stream)
         mark(0)
         if path == "forward":
-            model.stage_articulate(betas, pose, joints=joints)
+            model.stage_articulate(betas, pose, trans, joints=joints)
             mark(1)
-            model.stage_blend_skin(B, verts)
+            model.stage_blend_skin(B, verts, trans=trans)
             mark(2)
         elif path == "api":
-            model.forward(betas, pose, joints=True, out=out)
+            model.forward(betas, pose, trans, joints=True, out=out)
             mark(1)
         else:  # unfused: articulate, blend GEMM (v_posed to HBM), LBS
-            model.stage_articulate(betas, pose, joints=joints)
+            model.stage_articulate(betas, pose, trans, joints=joints)
             mark(1)
             model.stage_blend(B)
             mark(2)
-            model.stage_skin(B, verts)
+            model.stage_skin(B, verts, trans=trans)
             mark(3)
 
     n_marks = {"forward": 3, "api": 2, "unfused": 4}
 
     def step(marks=None):
         run_path(args.path, marks)
-        if args.gather and world > 1:
-            if args.backend == "nccl":  # RCCL over xGMI, device to device
-                gather_to_root(verts, B * world, root=0)
-                gather_to_root(joints, B * world, root=0)
-            else:
+        if gather and world > 1:
+            if gatherer is not None:  # RCCL over xGMI, peer -> GPU 0 sends
+                gatherer.gather(verts, B * world, root=0, out=gv)
+                gatherer.gather(joints, B * world, root=0, out=gj)
+            else:  # gloo rehearsal: the joints through the host
                 gather_to_root(joints.cpu(), B * world, root=0)
 
+    # Clock ramp, then the untimed warmup.
+    t_ramp = time.perf_counter()
+    n_ramp = 0
+    while True:
+        for _ in range(10):
+            step()
+        n_ramp += 10
+        torch.cuda.synchronize()
+        if time.perf_counter() - t_ramp >= args.ramp_seconds:
+            break
+    t_ramp = time.perf_counter() - t_ramp
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -200,7 +321,7 @@ def main():
     ms = {k: span(a, b, events) for k, (a, b) in timed[args.path].items()}
     other = {"fp32": "f16x3", "f16x3": "fp32"}[args.precision]
     ms_other = {}
-    if rank == 0:
+    if rank == 0 and not args.no_extra:
         def time_path(path, into, reps=50):
             evs = [[torch.cuda.Event(enable_timing=True) for _ in range(n_marks[path])]
                    for _ in range(reps)]
@@ -284,18 +405,25 @@ def main():
     # Roofline of the dominant kernel of the timed path.
     if args.path == "unfused":
         dominant = "blend" if ms["blend"] >= ms["skin"] else "skin"
+    elif args.path == "api":
+        dominant = "blend_skin" if "blend_skin" in kernels else None
     else:
         dominant = "blend_skin"
-    kd = kernels[dominant]
-    if kd["bound"] == "mfma":
-        roof = {"kernel": kd["kernel"], "bound": "mfma", "achieved": kd["achieved_TFLOPs"],
-                "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": kd["frac"]}
-    else:
-        roof = {"kernel": kd["kernel"], "bound": "hbm", "achieved": kd["achieved_GBs"],
-                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": kd["frac"]}
-    roof["traffic"] = load_traffic(args.pmc, dominant + ("_h3" if args.precision == "f16x3" else ""), B)
-    roof["algorithmic_per_hand"] = kd.get("flop_per_hand", kd.get("bytes_per_hand"))
-    roof["timed_in_region"] = dominant in in_path
+    roof = None
+    if dominant is not None:
+        kd = kernels[dominant]
+        if kd["bound"] == "mfma":
+            roof = {"kernel": kd["kernel"], "bound": "mfma", "achieved": kd["achieved_TFLOPs"],
+                    "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": kd["frac"]}
+        else:
+            roof = {"kernel": kd["kernel"], "bound": "hbm", "achieved": kd["achieved_GBs"],
+                    "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": kd["frac"]}
+        traffic, src = load_traffic(args.pmc, dominant + ("_h3" if args.precision == "f16x3" else ""), B)
+        roof["traffic"] = traffic
+        roof["traffic_source"] = src
+        roof["algorithmic_per_hand"] = kd.get("flop_per_hand", kd.get("bytes_per_hand"))
+        roof["hands_per_launch"] = B
+        roof["timed_in_region"] = dominant in in_path
 
     if rank == 0:
         total = B * world * args.steps
@@ -306,25 +434,31 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "ramp": {"seconds": t_ramp, "steps": n_ramp},
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": args.precision,
             "data": "synthetic (random-init MANO arrays of the official shapes, seed 0; "
-                    "beta ~ N(0,1), pose ~ N(0,0.5^2) rad, generated on device)",
-            "config": {"workload": "C2: full-pose fp32 MANO forward, 65,536 hands per GPU"
-                       if B == 65536 else f"{B} hands per GPU",
-                       "hands_per_gpu": B, "global_batch": B * world, "outputs": "verts+joints",
-                       "path": args.path,
-                       "gather_to_gpu0": bool(args.gather and world > 1),
+                    "Philox inputs keyed by (seed, global hand index): beta ~ N(0,1), "
+                    "pose ~ N(0,0.5^2) rad" + (", trans ~ U(-1,1) m" if with_trans else "") +
+                    ", generated on device)",
+            "config": {"workload": wl["desc"] if B == wl["hands"] else f"{args.workload} at {B} hands per GPU",
+                       "hands_per_gpu": B, "global_batch": B * world,
+                       "outputs": "verts+joints", "trans": with_trans, "path": args.path,
+                       "gather_to_gpu0": bool(gather and world > 1),
+                       "gather_impl": None if not (gather and world > 1) else
+                       ("mano_gather (RCCL send/recv)" if gatherer is not None else "gloo rehearsal"),
                        "parallelism": f"dp{world}"},
             "roofline": roof,
             "kernels": kernels,
         }
         if world == 1 and not args.no_cpu:
-            line["cpu_baseline"] = cpu_baseline(params, args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(args.cpu_procs or cpu_share(), args.cpu_seconds)
         print(json.dumps(line), flush=True)
+    if gatherer is not None:
+        gatherer.close()
     model.close()
     if world > 1:
         dist.destroy_process_group()

@@ -44,6 +44,7 @@ extern "C" {
 #define MANO_EHIP (-2)     /* HIP runtime error (allocation, copy, launch)      */
 #define MANO_ESMALL (-3)   /* workspace smaller than mano_workspace_bytes()     */
 #define MANO_ESTATE (-4)   /* handle destroyed / wrong device                   */
+#define MANO_ECOMM (-5)    /* RCCL unavailable or a collective failed           */
 
 #define MANO_N_JOINTS 16
 #define MANO_N_SHAPE 10
@@ -148,10 +149,78 @@ int mano_pose_from_pca(const mano_model* model, int64_t n_hands, const float* pc
                        int32_t n_comps, int64_t pca_stride, const float* rot,
                        int64_t rot_stride, float* pose, void* stream);
 
+/* set_params(pose_pca=..., global_rot=..., shape=...) (mano_np.py:48-77) for a
+ * batch: the PCA map of mano_pose_from_pca runs as the prologue of the
+ * articulation kernel (no pose round trip through HBM), then the forward
+ * pass of mano_forward.  pca [n][pca_stride] (stride 0 = one shared row,
+ * 0 <= n_comps <= 45; n_comps 0 gives the PCA mean), rot [n][3] (rot_stride 0
+ * = shared; NULL = zero root rotation, the reference's initial `rot`).
+ * pose_out (nullable) receives the [n][16][3] pose the kernels used -- bit for
+ * bit what mano_pose_from_pca returns.  Needs a model created with the PCA
+ * arrays.  Other arguments as mano_forward. */
+int mano_forward_pca(const mano_model* model, int64_t n_hands, const float* betas,
+                     int64_t betas_stride, const float* pca, int32_t n_comps,
+                     int64_t pca_stride, const float* rot, int64_t rot_stride,
+                     const float* trans, float* verts, float* joints, float* pose_out,
+                     float* rest_verts, float* rest_joints, float* rot_mats,
+                     void* workspace, size_t workspace_bytes, void* stream);
+
 /* MANOModel.rodrigues (mano_np.py:117-148): n axis-angle vectors [n][3] ->
  * rotation matrices [n][3][3]. */
 int mano_rodrigues(int device, int64_t n, const float* axis_angle, float* rot,
                    void* stream);
+
+/* ---- Device memory and streams without a framework --------------------
+ * So that the reference's own process (numpy + ctypes, no torch) can hold
+ * the device buffers mano_forward reads and writes.
+ * mano_alloc returns 256-byte aligned device memory on `device`;
+ * mano_memcpy copies `bytes` in direction `kind` (MANO_MEMCPY_*), on
+ * `stream` asynchronously, or synchronously when stream is NULL;
+ * mano_synchronize waits for every launch on `device`. */
+#define MANO_MEMCPY_HOST_TO_DEVICE 1
+#define MANO_MEMCPY_DEVICE_TO_HOST 2
+#define MANO_MEMCPY_DEVICE_TO_DEVICE 3
+int mano_alloc(int device, size_t bytes, void** out);
+int mano_free(int device, void* ptr);
+int mano_memcpy(int device, void* dst, const void* src, size_t bytes, int32_t kind,
+                void* stream);
+int mano_synchronize(int device);
+
+/* ---- Synthetic workload (benchmarks, shard-invariance tests) ------------
+ * Hand i of the batch is global hand first_index + i; its values are drawn
+ * by Philox-4x32-10 keyed by `seed` with counter (global index, block), so a
+ * shard [a, b) of a global batch reproduces exactly hands a..b-1 of the
+ * 1-GPU batch.  Per hand, 16 Philox blocks give
+ * 64 uint32 words w[0..63]: w[0..57] become 58 normals by Box-Muller on the
+ * pairs (w[2m], w[2m+1]) (cos for the even member, sin for the odd),
+ * betas [n][10] = beta_sigma * N[0..9], pose [n][16][3] = pose_sigma *
+ * N[10..57], trans [n][3] = trans_range * (2 u(w[58..60]) - 1), with
+ * u(w) = ((w >> 8) + 0.5) / 2^24 in (0, 1) and N = sqrt(-2 ln u(w[2m])) *
+ * (cos, sin)(2 pi u(w[2m+1])), evaluated in float32.  Each output is
+ * nullable. */
+int mano_synthetic_inputs(int device, uint64_t seed, int64_t first_index, int64_t n_hands,
+                          float beta_sigma, float pose_sigma, float trans_range,
+                          float* betas, float* pose, float* trans, void* stream);
+
+/* ---- Gather of per-rank shards to one GPU (RCCL over xGMI) --------------
+ * The forward has no collective (hands are independent); this assembles the
+ * shards of a data-parallel batch on `root` when the caller wants every
+ * vertex on one device (BASELINE config C4).  One rank per GPU and process;
+ * rank 0 makes the id with mano_comm_unique_id and hands it to the others
+ * out of band.  mano_gather is a grouped RCCL send/recv: every peer sends
+ * its `send_bytes` straight to root over its own xGMI link (no ring), root
+ * lands rank r's bytes at recv + sum(rank_bytes[0..r-1]) (rank_bytes: the
+ * per-rank sizes, read on root only; NULL = every rank sends send_bytes), so
+ * ragged contiguous shards need no padding.  recv is read on root only.
+ * Asynchronous on `stream`.  RCCL (librccl.so.1) is loaded on first use. */
+#define MANO_COMM_ID_BYTES 128
+typedef struct mano_comm mano_comm;
+int mano_comm_unique_id(unsigned char* id /* [MANO_COMM_ID_BYTES] */);
+int mano_comm_create(int device, int32_t n_ranks, int32_t rank, const unsigned char* id,
+                     mano_comm** out);
+int mano_comm_destroy(mano_comm* comm);
+int mano_gather(mano_comm* comm, const void* send, size_t send_bytes, void* recv,
+                const size_t* rank_bytes, int32_t root, void* stream);
 
 /* Message of the last failed call on this thread ("" if none). */
 const char* mano_last_error(void);

@@ -119,9 +119,17 @@ void split_f16(double x, uint16_t& hi, uint16_t& lo) {
 
 }  // namespace
 
+namespace mano {
+// The thread-local message of mano_last_error(), for the other ABI files.
+int set_error(int code, const char* msg) {
+  g_last_error = msg;
+  return code;
+}
+}  // namespace mano
+
 extern "C" {
 
-int mano_abi_version(void) { return 1; }
+int mano_abi_version(void) { return 2; }
 
 const char* mano_last_error(void) { return g_last_error.c_str(); }
 
@@ -331,6 +339,7 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   m->dm.h3_vposed_unscale = float(std::ldexp(1.0, -basis_exp));
   m->dm.h3_lbs_unscale = float(std::ldexp(1.0, -(kH3FrameExp + kH3WeightExp)));
   m->dm.precision = MANO_PRECISION_FP32;
+  m->dm.has_pca = pose_pca_basis != nullptr;
   m->dm.n_groups16 = n_groups16;
   m->dm.max_depth = max_depth;
   m->dm.n_verts = V;
@@ -502,6 +511,7 @@ int mano_pose_from_pca(const mano_model* m, int64_t n, const float* pca, int32_t
     return fail(MANO_EINVAL, "pca_stride %lld < n_comps %d", (long long)pca_stride, n_comps);
   if (rot_stride != 0 && rot_stride < 3)
     return fail(MANO_EINVAL, "rot_stride %lld must be 0 or >= 3", (long long)rot_stride);
+  if (!m->dm.has_pca) return fail(MANO_EINVAL, "the model was created without the PCA arrays");
   if (n == 0) return MANO_OK;
   if (!pose || (n_comps > 0 && !pca)) return fail(MANO_EINVAL, "pose / pca pointer is NULL");
   DeviceGuard guard(m->device);
@@ -509,6 +519,114 @@ int mano_pose_from_pca(const mano_model* m, int64_t n, const float* pca, int32_t
   hipError_t e = mano::launch_pose_from_pca(m->dm, n, pca, n_comps, pca_stride, rot, rot_stride,
                                             pose, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "pose_from_pca launch");
+  return MANO_OK;
+}
+
+int mano_forward_pca(const mano_model* m, int64_t n, const float* betas, int64_t betas_stride,
+                     const float* pca, int32_t n_comps, int64_t pca_stride, const float* rot,
+                     int64_t rot_stride, const float* trans, float* verts, float* joints,
+                     float* pose_out, float* rest_verts, float* rest_joints, float* rot_mats,
+                     void* ws, size_t ws_bytes, void* stream) {
+  g_last_error.clear();
+  if (int rc = check_model(m)) return rc;
+  if (n < 0 || n > kMaxHands) return fail(MANO_EINVAL, "n_hands %lld out of range", (long long)n);
+  if (!m->dm.has_pca) return fail(MANO_EINVAL, "the model was created without the PCA arrays");
+  if (n_comps < 0 || n_comps > mano::kPca)
+    return fail(MANO_EINVAL, "n_comps %d must be in [0, 45] (mano_np.py:55-56)", n_comps);
+  if (pca_stride != 0 && pca_stride < n_comps)
+    return fail(MANO_EINVAL, "pca_stride %lld < n_comps %d", (long long)pca_stride, n_comps);
+  if (rot_stride != 0 && rot_stride < 3)
+    return fail(MANO_EINVAL, "rot_stride %lld must be 0 or >= 3", (long long)rot_stride);
+  if (betas_stride != 0 && betas_stride < mano::kShape)
+    return fail(MANO_EINVAL, "betas_stride %lld must be 0 or >= 10", (long long)betas_stride);
+  if (n == 0) return MANO_OK;
+  if (!betas || !verts || (n_comps > 0 && !pca))
+    return fail(MANO_EINVAL, "betas, verts and (for n_comps > 0) pca are required");
+  if (int rc = check_workspace(m, n, ws, ws_bytes, false)) return rc;
+  DeviceGuard guard(m->device);
+  if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
+  const mano::Workspace w = mano::workspace_layout(m->dm, n);
+  char* base = static_cast<char*>(ws);
+  const mano::PcaInput in{pca, n_comps, pca_stride, rot, rot_stride, pose_out};
+  hipError_t e = mano::launch_articulate(
+      m->dm, n, betas, betas_stride, nullptr, trans, reinterpret_cast<float*>(base + w.features_off),
+      reinterpret_cast<float*>(base + w.transforms_off), joints, rest_joints, rot_mats,
+      static_cast<hipStream_t>(stream), &in);
+  if (e != hipSuccess) return hip_fail(e, "articulate (pca) launch");
+  return mano_stage_blend_skin(m, n, rest_verts, trans, verts, ws, ws_bytes, stream);
+}
+
+// ---- device memory and streams without a framework ----
+int mano_alloc(int device, size_t bytes, void** out) {
+  g_last_error.clear();
+  if (!out) return fail(MANO_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (device < 0) return fail(MANO_EINVAL, "device %d is negative", device);
+  DeviceGuard guard(device);
+  if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
+  if (bytes == 0) return MANO_OK;
+  hipError_t e = hipMalloc(out, bytes);  // 256-B aligned (hipMalloc granularity)
+  if (e != hipSuccess) {
+    *out = nullptr;
+    return hip_fail(e, "hipMalloc");
+  }
+  return MANO_OK;
+}
+
+int mano_free(int device, void* ptr) {
+  g_last_error.clear();
+  if (!ptr) return MANO_OK;
+  if (device < 0) return fail(MANO_EINVAL, "device %d is negative", device);
+  DeviceGuard guard(device);
+  if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
+  hipError_t e = hipFree(ptr);
+  if (e != hipSuccess) return hip_fail(e, "hipFree");
+  return MANO_OK;
+}
+
+int mano_memcpy(int device, void* dst, const void* src, size_t bytes, int32_t kind, void* stream) {
+  g_last_error.clear();
+  hipMemcpyKind k;
+  switch (kind) {
+    case MANO_MEMCPY_HOST_TO_DEVICE: k = hipMemcpyHostToDevice; break;
+    case MANO_MEMCPY_DEVICE_TO_HOST: k = hipMemcpyDeviceToHost; break;
+    case MANO_MEMCPY_DEVICE_TO_DEVICE: k = hipMemcpyDeviceToDevice; break;
+    default: return fail(MANO_EINVAL, "memcpy kind %d is not a MANO_MEMCPY_* value", kind);
+  }
+  if (bytes == 0) return MANO_OK;
+  if (!dst || !src) return fail(MANO_EINVAL, "memcpy dst / src is NULL");
+  if (device < 0) return fail(MANO_EINVAL, "device %d is negative", device);
+  DeviceGuard guard(device);
+  if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
+  hipError_t e = stream ? hipMemcpyAsync(dst, src, bytes, k, static_cast<hipStream_t>(stream))
+                        : hipMemcpy(dst, src, bytes, k);
+  if (e != hipSuccess) return hip_fail(e, "hipMemcpy");
+  return MANO_OK;
+}
+
+int mano_synchronize(int device) {
+  g_last_error.clear();
+  if (device < 0) return fail(MANO_EINVAL, "device %d is negative", device);
+  DeviceGuard guard(device);
+  if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
+  return MANO_OK;
+}
+
+int mano_synthetic_inputs(int device, uint64_t seed, int64_t first, int64_t n, float beta_sigma,
+                          float pose_sigma, float trans_range, float* betas, float* pose,
+                          float* trans, void* stream) {
+  g_last_error.clear();
+  if (n < 0 || n > kMaxHands) return fail(MANO_EINVAL, "n_hands %lld out of range", (long long)n);
+  if (first < 0) return fail(MANO_EINVAL, "first_index %lld < 0", (long long)first);
+  if (device < 0) return fail(MANO_EINVAL, "device %d is negative", device);
+  if (n == 0 || (!betas && !pose && !trans)) return MANO_OK;
+  DeviceGuard guard(device);
+  if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
+  hipError_t e = mano::launch_synthetic_inputs(seed, first, n, beta_sigma, pose_sigma, trans_range,
+                                               betas, pose, trans, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "synthetic_inputs launch");
   return MANO_OK;
 }
 

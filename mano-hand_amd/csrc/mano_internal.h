@@ -90,6 +90,7 @@ struct DeviceModel {
   float h3_vposed_unscale;  // 2^-basis_exp: GEMM accumulator -> v_posed
   float h3_lbs_unscale;     // 2^-(kH3FrameExp + kH3WeightExp): LBS sum -> verts
   int32_t precision;    // MANO_PRECISION_* of mano_forward / blend_skin / skin
+  int32_t has_pca;      // created with pose_pca_basis / pose_pca_mean
   int32_t max_depth;
   int32_t n_verts;
   int32_t n_cols;       // 3V
@@ -114,11 +115,24 @@ inline Workspace workspace_layout(const DeviceModel& m, int64_t n) {
   return w;
 }
 
+// PCA pose input of the articulation (mano_forward_pca): pose = [rot |
+// pca[:n_comps] . pose_pca_basis[:n_comps] + mean] (mano_np.py:66-72).
+struct PcaInput {
+  const float* pca;
+  int32_t n_comps;
+  int64_t pca_stride;
+  const float* rot;      // nullable: zero root rotation
+  int64_t rot_stride;
+  float* pose_out;       // nullable: the [n][16][3] pose used
+};
+
 // Kernel launchers (mano_kernels.hip).  All asynchronous on `stream`.
+// `pca` non-NULL: the pose comes from PCA coefficients (`pose` unused).
 hipError_t launch_articulate(const DeviceModel& m, int64_t n, const float* betas,
                              int64_t betas_stride, const float* pose, const float* trans,
                              float* features, float* transforms, float* joints,
-                             float* rest_joints, float* rot_mats, hipStream_t stream);
+                             float* rest_joints, float* rot_mats, hipStream_t stream,
+                             const PcaInput* pca = nullptr);
 hipError_t launch_blend(const DeviceModel& m, int64_t n, const float* features,
                         float* vposed, hipStream_t stream);
 hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features,
@@ -139,5 +153,8 @@ hipError_t launch_pose_from_pca(const DeviceModel& m, int64_t n, const float* pc
                                 int n_comps, int64_t pca_stride, const float* rot,
                                 int64_t rot_stride, float* pose, hipStream_t stream);
 hipError_t launch_rodrigues(int64_t n, const float* aa, float* rot, hipStream_t stream);
+hipError_t launch_synthetic_inputs(uint64_t seed, int64_t first, int64_t n, float beta_sigma,
+                                   float pose_sigma, float trans_range, float* betas, float* pose,
+                                   float* trans, hipStream_t stream);
 
 }  // namespace mano

@@ -165,13 +165,40 @@ __device__ __forceinline__ void store_joint_outputs(int64_t h, int j, const floa
 // 10-KB dwordx4 stream; transforms and joints are stored straight from the
 // lanes (48 and 12 contiguous bytes each).
 // ---------------------------------------------------------------------------
+// PCA pose of one (hand, joint) lane (set_params' PCA branch, mano_np.py:66-72):
+// joint 0 takes the global rotation, joint j >= 1 the three entries
+// 3 (j - 1) + c of c . basis[:N] + mean.  Same operation order as
+// pose_from_pca_kernel (fmaf chain over i, then + mean), so the fused and the
+// standalone PCA maps agree bit for bit.
+__device__ __forceinline__ void pca_joint_pose(const PcaInput& in, const float* __restrict__ basis,
+                                               const float* __restrict__ mean, int64_t h, int j,
+                                               float (&aa)[3]) {
+  if (j == 0) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) aa[c] = in.rot ? in.rot[h * in.rot_stride + c] : 0.f;
+    return;
+  }
+  const float* coef = in.pca + h * in.pca_stride;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const int mm = 3 * (j - 1) + c;
+    float v = 0.f;
+    for (int i = 0; i < in.n_comps; ++i) v = fmaf(coef[i], basis[i * kPca + mm], v);
+    aa[c] = v + mean[mm];
+  }
+}
+
+// kPca: the pose comes from PCA coefficients (pca_joint_pose prologue, the
+// basis rows in use staged in LDS) instead of the axis-angle `pose` input.
+template <bool kPca>
 __global__ __launch_bounds__(256) void articulate_kernel(
     const float* __restrict__ betas, int64_t betas_stride, const float* __restrict__ pose,
     const float* __restrict__ trans, const float* __restrict__ joint_template,
     const float* __restrict__ joint_shape, const int32_t* __restrict__ parents,
     const int32_t* __restrict__ depth, int max_depth, int64_t n,
     float* __restrict__ features, float* __restrict__ transforms, float* __restrict__ joints,
-    float* __restrict__ rest_joints, float* __restrict__ rot_mats) {
+    float* __restrict__ rest_joints, float* __restrict__ rot_mats, PcaInput pca,
+    const float* __restrict__ pca_basis, const float* __restrict__ pca_mean) {
   __shared__ f32x4 xs4[16 * kXStride / 4];
   // The folded joint regressor (J = Jt + Js . beta, 528 floats), staged once
   // per block: each lane reads its joint's 33 values from LDS, not HBM/L2.
@@ -181,6 +208,15 @@ __global__ __launch_bounds__(256) void articulate_kernel(
   const int tid = threadIdx.x;
   for (int i = tid; i < kJoints * 3 * kShape; i += 256) js_s[i] = joint_shape[i];
   if (tid < kJoints * 3) jt_s[tid] = joint_template[tid];
+  const float* basis_s = nullptr;
+  const float* mean_s = nullptr;
+  if constexpr (kPca) {
+    __shared__ float pb_s[kPca * kPca + kPca];
+    for (int i = tid; i < pca.n_comps * kPca; i += 256) pb_s[i] = pca_basis[i];
+    if (tid < kPca) pb_s[kPca * kPca + tid] = pca_mean[tid];
+    basis_s = pb_s;
+    mean_s = pb_s + kPca * kPca;
+  }
   __syncthreads();
   const int j = tid & (kJoints - 1);
   const int hl = tid >> 4;
@@ -188,14 +224,26 @@ __global__ __launch_bounds__(256) void articulate_kernel(
   const int64_t h = min(h0 + hl, n - 1);  // tail lanes repeat the last hand
   const bool valid = h0 + hl < n;
 
-  const float* p = pose + h * (kJoints * 3) + 3 * j;
+  float aa[3];
+  if constexpr (kPca) {
+    pca_joint_pose(pca, basis_s, mean_s, h, j, aa);
+    if (valid && pca.pose_out) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) pca.pose_out[h * (kJoints * 3) + 3 * j + c] = aa[c];
+    }
+  } else {
+    const float* p = pose + h * (kJoints * 3) + 3 * j;
+    aa[0] = p[0];
+    aa[1] = p[1];
+    aa[2] = p[2];
+  }
   float beta[kShape];
 #pragma unroll
   for (int s = 0; s < kShape; ++s) beta[s] = betas[h * betas_stride + s];
   const int par = parents[j];
   const int src = ((tid & 63) & ~(kJoints - 1)) + (par < 0 ? 0 : par);
   float rm[9], J[3], t[3], Aj[12];
-  articulate_joint(p[0], p[1], p[2], beta, j, src, depth[j], max_depth, jt_s, js_s, rm, J, t, Aj);
+  articulate_joint(aa[0], aa[1], aa[2], beta, j, src, depth[j], max_depth, jt_s, js_s, rm, J, t, Aj);
   if (valid) {
     f32x4* A = reinterpret_cast<f32x4*>(transforms + h * kTransformFloats + j * 12);
     A[0] = f32x4{Aj[0], Aj[1], Aj[2], Aj[3]};
@@ -713,16 +761,100 @@ __global__ __launch_bounds__(256) void rodrigues_kernel(const float* __restrict_
   for (int k = 0; k < 9; ++k) rot[9 * i + k] = rm[k] + ((k % 4 == 0) ? 1.f : 0.f);
 }
 
+// ---------------------------------------------------------------------------
+// Synthetic workload (include/mano_hip.h mano_synthetic_inputs): Philox-4x32-10
+// keyed by the seed, counter (global hand index lo, hi, block, 0).  One lane
+// per (hand, block): 16 lanes x 4 words = the hand's 64 words; Box-Muller pairs
+// (w[2m], w[2m+1]) never straddle a block.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void philox4x32_10(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r > 0) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const uint64_t p0 = uint64_t(0xD2511F53u) * c[0];
+    const uint64_t p1 = uint64_t(0xCD9E8D57u) * c[2];
+    const uint32_t hi0 = uint32_t(p0 >> 32), lo0 = uint32_t(p0);
+    const uint32_t hi1 = uint32_t(p1 >> 32), lo1 = uint32_t(p1);
+    c[0] = hi1 ^ c[1] ^ k0;
+    c[1] = lo1;
+    c[2] = hi0 ^ c[3] ^ k1;
+    c[3] = lo0;
+  }
+}
+
+// u in (0, 1), exactly representable: ((w >> 8) + 0.5) / 2^24.
+__device__ __forceinline__ float unit_open(uint32_t w) {
+  return (float(w >> 8) + 0.5f) * (1.0f / 16777216.0f);
+}
+
+__global__ __launch_bounds__(256) void synthetic_inputs_kernel(
+    uint32_t k0, uint32_t k1, int64_t first, int64_t n, float beta_sigma, float pose_sigma,
+    float trans_range, float* __restrict__ betas, float* __restrict__ pose,
+    float* __restrict__ trans) {
+  const int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  const int64_t h = idx >> 4;
+  const int b = int(idx & 15);
+  if (h >= n) return;
+  const uint64_t g = uint64_t(first + h);
+  uint32_t w[4] = {uint32_t(g), uint32_t(g >> 32), uint32_t(b), 0u};
+  philox4x32_10(w, k0, k1);
+#pragma unroll
+  for (int pr = 0; pr < 2; ++pr) {
+    const int e = 4 * b + 2 * pr;  // element index of the pair's first member
+    float v[2];
+    if (e < 58) {
+      const float r = sqrtf(-2.0f * logf(unit_open(w[2 * pr])));
+      float s, c;
+      sincospif(2.0f * unit_open(w[2 * pr + 1]), &s, &c);
+      v[0] = r * c;
+      v[1] = r * s;
+    } else {
+      v[0] = 2.0f * unit_open(w[2 * pr]) - 1.0f;
+      v[1] = 2.0f * unit_open(w[2 * pr + 1]) - 1.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int el = e + q;
+      if (el < kShape) {
+        if (betas) betas[h * kShape + el] = beta_sigma * v[q];
+      } else if (el < 58) {
+        if (pose) pose[h * (kJoints * 3) + (el - kShape)] = pose_sigma * v[q];
+      } else if (el < 61) {
+        if (trans) trans[h * 3 + (el - 58)] = trans_range * v[q];
+      }
+    }
+  }
+}
+
 }  // namespace
+
+hipError_t launch_synthetic_inputs(uint64_t seed, int64_t first, int64_t n, float beta_sigma,
+                                   float pose_sigma, float trans_range, float* betas, float* pose,
+                                   float* trans, hipStream_t stream) {
+  const int64_t threads = n * 16;
+  hipLaunchKernelGGL(synthetic_inputs_kernel, dim3(unsigned((threads + 255) / 256)), dim3(256), 0,
+                     stream, uint32_t(seed), uint32_t(seed >> 32), first, n, beta_sigma, pose_sigma,
+                     trans_range, betas, pose, trans);
+  return hipGetLastError();
+}
 
 hipError_t launch_articulate(const DeviceModel& m, int64_t n, const float* betas,
                              int64_t betas_stride, const float* pose, const float* trans,
                              float* features, float* transforms, float* joints,
-                             float* rest_joints, float* rot_mats, hipStream_t stream) {
+                             float* rest_joints, float* rot_mats, hipStream_t stream,
+                             const PcaInput* pca) {
   const int64_t blocks = (n + 15) / 16;
-  hipLaunchKernelGGL(articulate_kernel, dim3(unsigned(blocks)), dim3(256), 0, stream, betas,
-                     betas_stride, pose, trans, m.joint_template, m.joint_shape, m.parents,
-                     m.depth, m.max_depth, n, features, transforms, joints, rest_joints, rot_mats);
+  auto launch = [&](auto kernel, const PcaInput& in) {
+    hipLaunchKernelGGL(kernel, dim3(unsigned(blocks)), dim3(256), 0, stream, betas, betas_stride,
+                       pose, trans, m.joint_template, m.joint_shape, m.parents, m.depth,
+                       m.max_depth, n, features, transforms, joints, rest_joints, rot_mats, in,
+                       m.pca_basis, m.pca_mean);
+  };
+  if (pca) launch(articulate_kernel<true>, *pca);
+  else launch(articulate_kernel<false>, PcaInput{});
   return hipGetLastError();
 }
 

@@ -8,8 +8,8 @@ Drop-in for reyuwei/MANO-Hand's `mano_np.MANOModel`:
 
 Batched device API: `ManoHip(params).forward(betas, pose, trans)`.
 """
-from .model_io import (MANO_PARENTS, MODEL_KEYS, dump_model, load_dump, load_official,  # noqa: F401
-                       params_digest, save_dump, synthetic_params)
+from .model_io import (MANO_PARENTS, MODEL_KEYS, dump_model, dump_scans, load_dump,  # noqa: F401
+                       load_official, params_digest, save_dump, scans_to_pose, synthetic_params)
 
 
 def __getattr__(name):
@@ -21,5 +21,5 @@ def __getattr__(name):
 
 
 __all__ = ["MANOModel", "ManoHip", "write_obj", "load_dump", "save_dump", "synthetic_params",
-           "load_official", "dump_model",
+           "load_official", "dump_model", "dump_scans", "scans_to_pose",
            "params_digest", "MANO_PARENTS", "MODEL_KEYS"]

@@ -14,7 +14,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmano_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "mano_hip.h")
 
-MANO_OK, MANO_EINVAL, MANO_EHIP, MANO_ESMALL, MANO_ESTATE = 0, -1, -2, -3, -4
+MANO_OK, MANO_EINVAL, MANO_EHIP, MANO_ESMALL, MANO_ESTATE, MANO_ECOMM = 0, -1, -2, -3, -4, -5
+MANO_MEMCPY_HOST_TO_DEVICE, MANO_MEMCPY_DEVICE_TO_HOST, MANO_MEMCPY_DEVICE_TO_DEVICE = 1, 2, 3
+MANO_COMM_ID_BYTES = 128
 MANO_PRECISION_FP32, MANO_PRECISION_F16X3 = 0, 1
 PRECISIONS = {"fp32": MANO_PRECISION_FP32, "f16x3": MANO_PRECISION_F16X3}
 _CODE_NAMES = {MANO_EINVAL: "MANO_EINVAL", MANO_EHIP: "MANO_EHIP",
@@ -60,7 +62,19 @@ SIGNATURES = {
     "mano_stage_skin": (ctypes.c_int, [_p, _i64, _p, _p, _p, _p, ctypes.c_size_t, _p]),
     "mano_stage_blend_skin": (ctypes.c_int, [_p, _i64, _p, _p, _p, _p, ctypes.c_size_t, _p]),
     "mano_pose_from_pca": (ctypes.c_int, [_p, _i64, _p, _i32, _i64, _p, _i64, _p, _p]),
+    "mano_forward_pca": (ctypes.c_int, [_p, _i64, _p, _i64, _p, _i32, _i64, _p, _i64, _p, _p, _p,
+                                        _p, _p, _p, _p, _p, ctypes.c_size_t, _p]),
     "mano_rodrigues": (ctypes.c_int, [ctypes.c_int, _i64, _p, _p, _p]),
+    "mano_alloc": (ctypes.c_int, [ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(_p)]),
+    "mano_free": (ctypes.c_int, [ctypes.c_int, _p]),
+    "mano_memcpy": (ctypes.c_int, [ctypes.c_int, _p, _p, ctypes.c_size_t, _i32, _p]),
+    "mano_synchronize": (ctypes.c_int, [ctypes.c_int]),
+    "mano_synthetic_inputs": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, _i64, _i64, ctypes.c_float,
+                                             ctypes.c_float, ctypes.c_float, _p, _p, _p, _p]),
+    "mano_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
+    "mano_comm_create": (ctypes.c_int, [ctypes.c_int, _i32, _i32, ctypes.c_char_p, ctypes.POINTER(_p)]),
+    "mano_comm_destroy": (ctypes.c_int, [_p]),
+    "mano_gather": (ctypes.c_int, [_p, _p, ctypes.c_size_t, _p, ctypes.POINTER(ctypes.c_size_t), _i32, _p]),
 }
 
 _LIB = None

@@ -10,10 +10,14 @@ wants the whole batch.
 """
 from __future__ import annotations
 
+import ctypes
+import math
 from typing import Optional, Tuple
 
 import torch
 import torch.distributed as dist
+
+from . import _abi
 
 
 def shard_range(n_total: int, rank: int, world: int) -> Tuple[int, int]:
@@ -44,6 +48,8 @@ def gather_to_root(shard: torch.Tensor, n_total: int, root: int = 0,
         return shard
     per = -(-n_total // world)
     start, stop = shard_range(n_total, rank, world)
+    # `root` is a rank of `group`; torch's gather takes a global rank.
+    dst = root if group is None else dist.get_global_rank(group, root)
     if shard.shape[0] != stop - start:
         raise ValueError(f"rank {rank} shard has {shard.shape[0]} rows, expected {stop - start}")
     if shard.shape[0] == per:
@@ -53,9 +59,9 @@ def gather_to_root(shard: torch.Tensor, n_total: int, root: int = 0,
         send[: shard.shape[0]] = shard
     if rank == root:
         full = shard.new_empty((per * world,) + tuple(shard.shape[1:]))
-        dist.gather(send, gather_list=list(full.chunk(world, 0)), dst=root, group=group)
+        dist.gather(send, gather_list=list(full.chunk(world, 0)), dst=dst, group=group)
         return full[:n_total]
-    dist.gather(send, gather_list=None, dst=root, group=group)
+    dist.gather(send, gather_list=None, dst=dst, group=group)
     return None
 
 
@@ -70,3 +76,51 @@ def all_gather(shard: torch.Tensor, n_total: int, group=None) -> torch.Tensor:
     full = shard.new_empty((per * world,) + tuple(shard.shape[1:]))
     dist.all_gather_into_tensor(full, send, group=group)
     return full[:n_total]
+
+
+class AbiGather:
+    """The C-ABI gather (include/mano_hip.h mano_comm_* / mano_gather): one
+    RCCL group of direct peer -> root sends over xGMI, ragged shards landing
+    contiguously on root (no padding, no ring).  torch.distributed is used only
+    to hand rank 0's RCCL id to the other ranks."""
+
+    def __init__(self, device: int, group=None):
+        world, rank = _world(group)
+        self.world, self.rank, self.device = world, rank, device
+        lib = _abi.lib()
+        uid = ctypes.create_string_buffer(_abi.MANO_COMM_ID_BYTES)
+        if rank == 0:
+            _abi.check(lib.mano_comm_unique_id(uid))
+        if world > 1:
+            box = [uid.raw]
+            dist.broadcast_object_list(box, src=0 if group is None else dist.get_global_rank(group, 0),
+                                       group=group)
+            uid = ctypes.create_string_buffer(box[0], _abi.MANO_COMM_ID_BYTES)
+        self._c = ctypes.c_void_p()
+        _abi.check(lib.mano_comm_create(device, world, rank, uid, ctypes.byref(self._c)))
+
+    def gather(self, shard: torch.Tensor, n_total: int, root: int = 0, out: Optional[torch.Tensor] = None,
+               stream=None) -> Optional[torch.Tensor]:
+        """Every rank passes its `shard_range` shard (dim 0); `root` gets the
+        (n_total, ...) tensor (into `out` when given), the others None."""
+        start, stop = shard_range(n_total, self.rank, self.world)
+        if shard.shape[0] != stop - start or not shard.is_contiguous():
+            raise ValueError(f"rank {self.rank} shard must be contiguous with {stop - start} rows")
+        row = math.prod(shard.shape[1:]) * shard.element_size()  # bytes per hand
+        sizes = (ctypes.c_size_t * self.world)(
+            *[(b - a) * row for a, b in (shard_range(n_total, r, self.world) for r in range(self.world))])
+        s = stream if stream is not None else torch.cuda.current_stream(shard.device)
+        full = None
+        if self.rank == root:
+            full = out if out is not None else torch.empty((n_total,) + tuple(shard.shape[1:]),
+                                                            dtype=shard.dtype, device=shard.device)
+        _abi.check(_abi.lib().mano_gather(
+            self._c, ctypes.c_void_p(shard.data_ptr()), shard.shape[0] * row,
+            None if full is None else ctypes.c_void_p(full.data_ptr()), sizes, root,
+            ctypes.c_void_p(s.cuda_stream)))
+        return full
+
+    def close(self):
+        if getattr(self, "_c", None) is not None and self._c.value:
+            _abi.check(_abi.lib().mano_comm_destroy(self._c))
+            self._c = None

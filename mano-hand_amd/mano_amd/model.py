@@ -86,7 +86,7 @@ class ManoHip:
             None if pca is None else _dptr(pca), None if mean is None else _dptr(mean),
             ctypes.byref(handle)))
         self._h = handle
-        self._ws = None
+        self._ws: Dict[int, torch.Tensor] = {}  # stream handle -> workspace
         self.set_precision(precision)
 
     def set_precision(self, precision: str) -> None:
@@ -117,18 +117,29 @@ class ManoHip:
                                                      ctypes.byref(c)))
         return a.value, b.value, c.value
 
-    def workspace(self, n: int, forward_only: bool = False) -> torch.Tensor:
-        """Cached device workspace large enough for `n` hands (all stage calls,
-        or with `forward_only` just mano_forward's X rows + transforms)."""
+    def workspace(self, n: int, forward_only: bool = False, stream=None) -> torch.Tensor:
+        """Device workspace large enough for `n` hands (all stage calls, or with
+        `forward_only` just mano_forward's X rows + transforms), one per stream.
+
+        Launches on different streams never share a workspace (the header's
+        rule for concurrent calls), and each workspace is allocated ON its
+        stream, so when it grows the caching allocator hands the old block out
+        again only in that stream's order -- never while a queued launch on the
+        stream may still read it."""
         lib = _abi.lib()
         need = int(lib.mano_forward_workspace_bytes(self._h, n) if forward_only
                    else lib.mano_workspace_bytes(self._h, n))
-        if self._ws is None or self._ws.numel() < need + 256:
-            self._ws = torch.empty(max(need, 256) + 256, dtype=torch.uint8, device=self.device)
-        return self._ws
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        key = s.cuda_stream
+        ws = self._ws.get(key)
+        if ws is None or ws.numel() < need + 256:
+            with torch.cuda.stream(s):
+                ws = torch.empty(max(need, 256) + 256, dtype=torch.uint8, device=self.device)
+            self._ws[key] = ws
+        return ws
 
-    def _ws_args(self, n, forward_only: bool = False):
-        ws = self.workspace(n, forward_only)
+    def _ws_args(self, n, forward_only: bool = False, stream=None):
+        ws = self.workspace(n, forward_only, stream)
         base = ws.data_ptr()
         aligned = (base + 255) & ~255
         return ctypes.c_void_p(aligned), ctypes.c_size_t(ws.numel() - (aligned - base))
@@ -162,6 +173,22 @@ class ManoHip:
         return B, betas, bstride, pose, trans
 
     # --------------------------------------------------------------- forward
+    def _outputs(self, out, stream, specs):
+        """Output tensors: the caller's (checked) or new ones allocated on the
+        launch stream (so the caching allocator orders their reuse after it)."""
+        res = dict(out) if out else {}
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        for name, shape, want in specs:
+            if not want:
+                continue
+            t = res.get(name)
+            if t is None:
+                with torch.cuda.stream(s):
+                    t = torch.empty(shape, dtype=torch.float32, device=self.device)
+                res[name] = t
+            self._check(t, name, shape)
+        return res
+
     def forward(self, betas: torch.Tensor, pose: torch.Tensor, trans: Optional[torch.Tensor] = None,
                 *, joints: bool = True, rest_verts: bool = False, rest_joints: bool = False,
                 rot_mats: bool = False, out: Optional[Dict[str, torch.Tensor]] = None,
@@ -175,44 +202,91 @@ class ManoHip:
         """
         B, betas, bstride, pose, trans = self._inputs(betas, pose, trans)
         V = self.n_verts
-        res = dict(out) if out else {}
-
-        def buf(name, shape, want):
-            if not want:
-                return None
-            t = res.get(name)
-            if t is None:
-                t = torch.empty(shape, dtype=torch.float32, device=self.device)
-                res[name] = t
-            return self._check(t, name, shape)
-
-        v = buf("verts", (B, V, 3), True)
-        j = buf("joints", (B, N_JOINTS, 3), joints)
-        rv = buf("rest_verts", (B, V, 3), rest_verts)
-        rj = buf("rest_joints", (B, N_JOINTS, 3), rest_joints)
-        rm = buf("rot_mats", (B, N_JOINTS, 3, 3), rot_mats)
-        ws, wsb = self._ws_args(B, forward_only=True)
+        res = self._outputs(out, stream, (
+            ("verts", (B, V, 3), True), ("joints", (B, N_JOINTS, 3), joints),
+            ("rest_verts", (B, V, 3), rest_verts), ("rest_joints", (B, N_JOINTS, 3), rest_joints),
+            ("rot_mats", (B, N_JOINTS, 3, 3), rot_mats)))
+        g = lambda k: _ptr(res.get(k))  # noqa: E731
+        ws, wsb = self._ws_args(B, forward_only=True, stream=stream)
         _abi.check(_abi.lib().mano_forward(
-            self._h, B, _ptr(betas), bstride, _ptr(pose), _ptr(trans), _ptr(v), _ptr(j), _ptr(rv),
-            _ptr(rj), _ptr(rm), ws, wsb, _stream_handle(self.device, stream)))
+            self._h, B, _ptr(betas), bstride, _ptr(pose), _ptr(trans), g("verts"),
+            g("joints") if joints else None, g("rest_verts") if rest_verts else None,
+            g("rest_joints") if rest_joints else None, g("rot_mats") if rot_mats else None,
+            ws, wsb, _stream_handle(self.device, stream)))
+        return res
+
+    def forward_pca(self, betas: torch.Tensor, pca: torch.Tensor, rot: Optional[torch.Tensor] = None,
+                    trans: Optional[torch.Tensor] = None, *, joints: bool = True,
+                    pose: bool = False, rest_verts: bool = False, rest_joints: bool = False,
+                    rot_mats: bool = False, out: Optional[Dict[str, torch.Tensor]] = None,
+                    stream=None) -> Dict[str, torch.Tensor]:
+        """Batched set_params(pose_pca=c, global_rot=rot, shape=beta)
+        (mano_np.py:66-77): the PCA map runs as the articulation prologue.
+
+        pca (B,N) (0 <= N <= 45) or (N,) shared, rot (B,3) / (3,) shared / None
+        (zero root rotation), betas as in `forward`.  `pose=True` also returns
+        the (B,16,3) pose the kernels used."""
+        if not isinstance(pca, torch.Tensor):
+            raise TypeError("pca must be a torch tensor")
+        if pca.dim() == 1:
+            N = pca.shape[0]
+            pca_stride = 0
+        else:
+            N = pca.shape[1]
+            pca_stride = N
+        if not 0 <= N <= 45:
+            raise ValueError(f"pca has {N} coefficients; at most 45 (mano_np.py:55-56)")
+        B = pca.shape[0] if pca.dim() == 2 else (betas.shape[0] if betas.dim() == 2 else None)
+        if B is None:
+            raise ValueError("batch size unknown: give (B,N) pca or (B,10) betas")
+        self._check(pca, "pose_pca", tuple(pca.shape))
+        if pca.dim() == 2 and pca.shape[0] != B:
+            raise ValueError("pca rows must match the batch")
+        if betas.dim() == 1:
+            betas = self._check(betas, "betas", (N_SHAPE,))
+            bstride = 0
+        else:
+            betas = self._check(betas, "betas", (B, N_SHAPE))
+            bstride = N_SHAPE
+        rot_stride = 0
+        if rot is not None:
+            if rot.dim() == 1 or (rot.dim() == 2 and rot.shape[0] == 1):
+                rot = self._check(rot.reshape(3), "global_rot", (3,))
+            else:
+                rot = self._check(rot, "global_rot", (B, 3))
+                rot_stride = 3
+        trans = self._check(trans, "trans", (B, 3))
+        V = self.n_verts
+        res = self._outputs(out, stream, (
+            ("verts", (B, V, 3), True), ("joints", (B, N_JOINTS, 3), joints),
+            ("pose", (B, N_JOINTS, 3), pose),
+            ("rest_verts", (B, V, 3), rest_verts), ("rest_joints", (B, N_JOINTS, 3), rest_joints),
+            ("rot_mats", (B, N_JOINTS, 3, 3), rot_mats)))
+        g = lambda k, want: _ptr(res.get(k)) if want else None  # noqa: E731
+        ws, wsb = self._ws_args(B, forward_only=True, stream=stream)
+        _abi.check(_abi.lib().mano_forward_pca(
+            self._h, B, _ptr(betas), bstride, _ptr(pca), N, pca_stride, _ptr(rot), rot_stride,
+            _ptr(trans), g("verts", True), g("joints", joints), g("pose", pose),
+            g("rest_verts", rest_verts), g("rest_joints", rest_joints), g("rot_mats", rot_mats),
+            ws, wsb, _stream_handle(self.device, stream)))
         return res
 
     # ---- the forward pass as separate kernels (per-kernel timing / intermediates) ----
     def stage_articulate(self, betas, pose, trans=None, joints=None, rest_joints=None,
                          rot_mats=None, stream=None):
         B, betas, bstride, pose, trans = self._inputs(betas, pose, trans)
-        ws, wsb = self._ws_args(B)
+        ws, wsb = self._ws_args(B, stream=stream)
         _abi.check(_abi.lib().mano_stage_articulate(
             self._h, B, _ptr(betas), bstride, _ptr(pose), _ptr(trans), _ptr(joints),
             _ptr(rest_joints), _ptr(rot_mats), ws, wsb, _stream_handle(self.device, stream)))
 
     def stage_blend(self, n: int, rest_verts=None, stream=None):
-        ws, wsb = self._ws_args(n)
+        ws, wsb = self._ws_args(n, stream=stream)
         _abi.check(_abi.lib().mano_stage_blend(self._h, n, _ptr(rest_verts), ws, wsb,
                                                _stream_handle(self.device, stream)))
 
     def stage_skin(self, n: int, verts: torch.Tensor, rest_verts=None, trans=None, stream=None):
-        ws, wsb = self._ws_args(n)
+        ws, wsb = self._ws_args(n, stream=stream)
         _abi.check(_abi.lib().mano_stage_skin(self._h, n, _ptr(rest_verts), _ptr(trans),
                                               _ptr(verts), ws, wsb,
                                               _stream_handle(self.device, stream)))
@@ -220,18 +294,18 @@ class ManoHip:
     def stage_blend_skin(self, n: int, verts: torch.Tensor, rest_verts=None, trans=None,
                          stream=None):
         """Fused blend GEMM + LBS (the second half of `forward`)."""
-        ws, wsb = self._ws_args(n)
+        ws, wsb = self._ws_args(n, stream=stream)
         _abi.check(_abi.lib().mano_stage_blend_skin(self._h, n, _ptr(rest_verts), _ptr(trans),
                                                     _ptr(verts), ws, wsb,
                                                     _stream_handle(self.device, stream)))
 
-    def intermediates(self, n: int) -> Dict[str, torch.Tensor]:
+    def intermediates(self, n: int, stream=None) -> Dict[str, torch.Tensor]:
         """Views of the workspace after the stage calls over `n` hands:
         `features` (n, 160) the blend-GEMM A operand rows X = [beta | R-I
         features | 1 | 0...] in the kernels' k-permuted order (`X[:, k] =
         features[:, X_POS[k]]`), `transforms` (n,16,3,4) skinning transforms,
         `vposed` (n,V,3)."""
-        ws = self.workspace(n)
+        ws = self.workspace(n, stream=stream)
         base = ws.data_ptr()
         shift = ((base + 255) & ~255) - base
         fo, to, vo = self.workspace_offsets(n)
@@ -241,6 +315,27 @@ class ManoHip:
             "transforms": f32[to // 4: to // 4 + n * 192].view(n, N_JOINTS, 3, 4),
             "vposed": f32[vo // 4: vo // 4 + n * self.n_verts * 3].view(n, self.n_verts, 3),
         }
+
+    # ---- synthetic workload (benchmarks and shard-invariance tests) ----
+    def synthetic_inputs(self, seed: int, first: int, n: int, *, beta_sigma: float = 1.0,
+                         pose_sigma: float = 0.5, trans_range: float = 1.0, trans: bool = False,
+                         stream=None) -> Dict[str, torch.Tensor]:
+        """Hands first..first+n-1 of the counter-based (Philox) synthetic batch
+        keyed by `seed` (include/mano_hip.h mano_synthetic_inputs): betas
+        (n,10) ~ N(0, beta_sigma^2), pose (n,16,3) ~ N(0, pose_sigma^2), and
+        with `trans` (n,3) ~ U(-trans_range, trans_range).  Any shard of a
+        global batch reproduces the same hands bit for bit."""
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(s):
+            out = {"betas": torch.empty((n, N_SHAPE), dtype=torch.float32, device=self.device),
+                   "pose": torch.empty((n, N_JOINTS, 3), dtype=torch.float32, device=self.device)}
+            if trans:
+                out["trans"] = torch.empty((n, 3), dtype=torch.float32, device=self.device)
+        _abi.check(_abi.lib().mano_synthetic_inputs(
+            self.device.index, seed, first, n, beta_sigma, pose_sigma, trans_range,
+            _ptr(out["betas"]), _ptr(out["pose"]), _ptr(out.get("trans")),
+            _stream_handle(self.device, stream)))
+        return out
 
     # ---- set_params' PCA branch and the Rodrigues helper on device ----
     def pose_from_pca(self, pca: torch.Tensor, rot: Optional[torch.Tensor] = None,
@@ -322,8 +417,9 @@ class MANOModel:
         """Same semantics as mano_np.py:48-77, plus an optional translation.
 
         pose_abs: per-joint axis-angle, shape [16, 3] (or [48]); taken verbatim.
-        pose_pca: [N] PCA coefficients, 0 < N <= 45; pose = c.basis[:N] + mean
-          with the stored global rotation `rot` prepended.
+        pose_pca: [N] PCA coefficients, N <= 45; pose = c.basis[:N] + mean
+          with the stored global rotation `rot` prepended (host float64; the
+          batched device form is `ManoHip.forward_pca`).
         global_rot: only read on the pose_pca branch, then kept in `rot`.
         shape: the 10 shape coefficients.
         trans: (extension) global translation [3], kept in `trans`.
@@ -332,13 +428,16 @@ class MANOModel:
         if pose_abs is not None:
             self.pose = pose_abs
         if pose_pca is not None:
-            n = pose_pca.shape[0]  # AttributeError for a list, like mano_np.py:67
-            if not 0 < n <= 45:
-                raise ValueError(f"pose_pca has {n} coefficients; 0 < N <= 45 (mano_np.py:55-56)")
+            # Host float64, the reference's own arithmetic (mano_np.py:67-72), so
+            # `pose` keeps float64 values across later shape-only updates.  A
+            # list raises AttributeError (.shape), N > 45 a ValueError (the
+            # matmul), N = 0 gives the mean pose -- all as the reference does.
+            n = pose_pca.shape[0]
+            fingers = (np.expand_dims(pose_pca, 0) @ np.asarray(self.pose_pca_basis)[:n])[0]
+            fingers = np.reshape(fingers + self.pose_pca_mean, [self.n_joints - 1, 3])
             if global_rot is not None:
                 self.rot = np.reshape(global_rot, [1, 3])
-            pose = self.engine.pose_from_pca(self._dev(pose_pca)[None], self._dev(self.rot))
-            self.pose = pose[0].double().cpu().numpy()
+            self.pose = np.concatenate([self.rot, fingers], 0)
         if shape is not None:
             self.shape = shape
         if trans is not None:

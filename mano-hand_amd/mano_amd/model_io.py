@@ -235,6 +235,46 @@ def dump_model(src_path: str, dst_path: str) -> None:
     save_dump(load_official(src_path), dst_path)
 
 
+def _scan_poses(path: str) -> np.ndarray:
+    """One official pickle's captured hand poses: hands_coeffs . hands_components
+    + hands_mean, as (M, 15, 3) finger axis-angles (dump_model.py:25-30)."""
+    with open(path, "rb") as f:
+        data = _OfficialUnpickler(f, encoding="latin1").load()
+    if not isinstance(data, dict):
+        raise pickle.UnpicklingError("official model file does not hold a dict")
+    data = {_norm_key(k): v for k, v in data.items()}
+    basis = _as_array(data["hands_components"], "hands_components")
+    mean = _as_array(data["hands_mean"], "hands_mean")
+    coeffs = _as_array(data["hands_coeffs"], "hands_coeffs")
+    return np.reshape(np.matmul(coeffs, basis) + mean, [-1, N_JOINTS - 1, 3])
+
+
+# The right hand's scans are mirrored into the left hand's frame (dump_model.py:38).
+RIGHT_TO_LEFT = np.array([[[1, -1, -1]]])
+
+
+def dump_scans(left_path: str, right_path: str, dst_path: str = None) -> np.ndarray:
+    """dump_model.py:24-43 without chumpy: the captured scan poses of both
+    official pickles as one (M_left + M_right, 15, 3) array of finger
+    axis-angles (left, then right mirrored by [1, -1, -1]), saved with
+    `np.save` when `dst_path` is given (the reference writes axangles.npy).
+    This is the realistic pose source of data_explore.py:12-15."""
+    left = _scan_poses(left_path)
+    right = _scan_poses(right_path)
+    right *= RIGHT_TO_LEFT
+    axangles = np.concatenate([left, right])
+    if dst_path is not None:
+        np.save(dst_path, axangles)
+    return axangles
+
+
+def scans_to_pose(axangles) -> np.ndarray:
+    """(M, 15, 3) scan axis-angles -> (M, 16, 3) full poses with a zero global
+    rotation prepended, as data_explore.py:13 feeds them to set_params."""
+    a = np.asarray(axangles, dtype=np.float64).reshape(-1, N_JOINTS - 1, 3)
+    return np.concatenate([np.zeros((a.shape[0], 1, 3)), a], axis=1)
+
+
 def parents_to_int(parents) -> np.ndarray:
     """`parents` list with None at the root -> int32 array with -1 at the root."""
     return np.array([-1 if p is None else int(p) for p in parents], dtype=np.int32)

@@ -15,7 +15,7 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, n), n
         assert n in _abi.SIGNATURES, f"{n} declared in the header but not bound"
     assert set(_abi.SIGNATURES) == set(names)
-    assert lib.mano_abi_version() == 1
+    assert lib.mano_abi_version() == 2
 
 
 def test_library_is_gfx950_code_object():
@@ -62,3 +62,33 @@ def test_check_raises_with_message():
     with pytest.raises(_abi.ManoError) as ei:
         _abi.check(rc)
     assert ei.value.code == _abi.MANO_EINVAL
+
+
+def test_memory_and_workload_argument_checks():
+    """The framework-free memory calls refuse bad arguments before any HIP call."""
+    lib = _abi.lib()
+    assert lib.mano_alloc(0, 16, None) == _abi.MANO_EINVAL
+    out = ctypes.c_void_p()
+    assert lib.mano_alloc(-1, 16, ctypes.byref(out)) == _abi.MANO_EINVAL and out.value is None
+    assert lib.mano_free(0, None) == _abi.MANO_OK
+    assert lib.mano_memcpy(0, ctypes.c_void_p(16), ctypes.c_void_p(16), 4, 9, None) == _abi.MANO_EINVAL
+    assert "kind" in _abi.last_error()
+    assert lib.mano_memcpy(0, None, ctypes.c_void_p(16), 4, _abi.MANO_MEMCPY_HOST_TO_DEVICE,
+                           None) == _abi.MANO_EINVAL
+    assert lib.mano_memcpy(0, None, None, 0, _abi.MANO_MEMCPY_HOST_TO_DEVICE, None) == _abi.MANO_OK
+    assert lib.mano_synchronize(-1) == _abi.MANO_EINVAL
+    assert lib.mano_synthetic_inputs(0, 1, -1, 4, 1.0, 0.5, 1.0, None, None, None, None) == _abi.MANO_EINVAL
+    assert lib.mano_synthetic_inputs(0, 1, 0, 0, 1.0, 0.5, 1.0, None, None, None, None) == _abi.MANO_OK
+
+
+def test_forward_pca_and_comm_argument_checks():
+    lib = _abi.lib()
+    assert lib.mano_forward_pca(None, 1, None, 10, None, 9, 9, None, 0, None, None, None, None,
+                                None, None, None, None, 0, None) == _abi.MANO_EINVAL
+    out = ctypes.c_void_p()
+    uid = ctypes.create_string_buffer(_abi.MANO_COMM_ID_BYTES)
+    assert lib.mano_comm_create(0, 2, 2, uid, ctypes.byref(out)) == _abi.MANO_EINVAL
+    assert lib.mano_comm_create(0, 1, 0, None, ctypes.byref(out)) == _abi.MANO_EINVAL
+    assert lib.mano_comm_destroy(None) == _abi.MANO_OK
+    assert lib.mano_gather(None, None, 0, None, None, 0, None) == _abi.MANO_EINVAL
+    assert lib.mano_comm_unique_id(None) == _abi.MANO_EINVAL

@@ -1,0 +1,74 @@
+"""bench.py's launcher and bookkeeping, on CPU (no GPU work).
+
+`bench.py --gpus N` with no WORLD_SIZE must start N ranks itself (the
+driver's 1/2/4/8 scaling command); `--launch-check` runs the real launch path
+-- torch.distributed.run, one process per rank, gloo barrier -- and exits
+before any GPU call."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import bench  # noqa: E402
+
+
+def _last_json(out):
+    return json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_gpus_flag_launches_n_ranks(n):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(n),
+                        "--backend", "gloo", "--launch-check"], capture_output=True, text=True,
+                       timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = _last_json(r.stdout)
+    assert line["n_gpus"] == n and line["local_ranks_ok"]
+
+
+def test_launch_command_is_torchrun():
+    cmd = bench.launch_command(["--gpus", "4", "--steps", "3"], 4)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert cmd[-3:] == ["--gpus", "4", "--steps", "3"] or cmd[-4:-1] == ["--gpus", "4", "--steps"]
+
+
+def test_workloads_match_baseline_configs():
+    w = bench.WORKLOADS
+    assert w["C2"]["hands"] == 65536 and not w["C2"]["trans"]
+    assert w["C3"]["hands"] * 8 == 2 ** 24
+    assert w["C4"]["hands"] * 8 == 2 ** 22 and w["C4"]["gather"]
+    assert w["C5"]["hands"] == 2 ** 20 and w["C5"]["trans"]
+    assert bench.parse([]).workload == "C2"          # the metric's config (BASELINE configs[1])
+    assert bench.parse([]).gpus == 1
+
+
+def test_algorithmic_work_constants():
+    assert bench.BLEND_FLOP_PER_HAND == 676860
+    assert bench.FUSED_MFMA_FLOP_PER_HAND == 975612
+    assert bench.SKIN_BYTES_PER_HAND == 19440
+    assert bench.FUSED_BYTES_PER_HAND == 10744
+
+
+def test_traffic_lookup(tmp_path):
+    p = tmp_path / "t.json"
+    p.write_text(json.dumps({"kernels": {"blend_skin": [
+        {"batch": 65536, "hbm_bytes_per_launch": 6.5536e8},
+        {"batch": 1048576, "hbm_bytes_per_launch": 2.0 * 1048576 * 1e4}]}}))
+    t, src = bench.load_traffic(str(p), "blend_skin", 65536)
+    assert t == 6.5536e8 and "65536" in src
+    t, src = bench.load_traffic(str(p), "blend_skin", 2097152)   # per-hand bytes of the largest x B
+    assert t == pytest.approx(2.0 * 2097152 * 1e4) and "per-hand" in src
+    assert bench.load_traffic(str(p), "skin", 65536) == (None, None)
+    # round-1 single-batch form
+    p.write_text(json.dumps({"batch": 65536, "kernels": {"skin": {"hbm_bytes_per_launch": 5.0}}}))
+    assert bench.load_traffic(str(p), "skin", 65536)[0] == 5.0
+
+
+def test_cpu_share_bounded():
+    assert 1 <= bench.cpu_share() <= 16

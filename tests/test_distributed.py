@@ -67,3 +67,38 @@ def test_gather_world2(n_total):
     assert np.array_equal(results[0][0], expect)
     for r in range(world):
         assert np.array_equal(results[r][1], expect)
+
+
+def _subgroup_worker(rank, world, port, q):
+    """Ranks 1 and 2 form a subgroup; its rank 0 (global rank 1) is the root."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        group = dist.new_group([1, 2])
+        res = None
+        if rank in (1, 2):
+            g_rank = rank - 1
+            a, b = shard_range(5, g_rank, 2)
+            shard = torch.arange(a, b, dtype=torch.float32)[:, None]
+            full = gather_to_root(shard, 5, root=0, group=group)
+            res = None if full is None else full.numpy()
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_root_is_a_group_rank():
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_subgroup_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0] is None and got[2] is None
+    assert np.array_equal(got[1][:, 0], np.arange(5, dtype=np.float32))

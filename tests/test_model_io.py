@@ -169,3 +169,28 @@ def test_load_official_refuses_code(tmp_path):
     p.write_bytes(pickle.dumps({"hands_components": Evil()}, protocol=2))
     with pytest.raises(pickle.UnpicklingError):
         model_io.load_official(str(p))
+
+
+def _scan_fixture():
+    from conftest import GOLDEN
+    with np.load(os.path.join(GOLDEN, "mano_reference_scans.npz"), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def test_dump_scans_matches_reference(tmp_path):
+    """dump_scans (dump_model.py:24-43) on official-layout pickles, against the
+    reference's own output (tests/golden/make_scan_goldens.py ran it)."""
+    g = _scan_fixture()
+    paths = {}
+    for side in ("left", "right"):
+        official = {k: g[f"{side}_{k}"] for k in ("hands_components", "hands_mean", "hands_coeffs")}
+        paths[side] = str(tmp_path / f"MANO_{side.upper()}.pkl")
+        with open(paths[side], "wb") as f:
+            pickle.dump(official, f, protocol=2)
+    dst = str(tmp_path / "axangles.npy")
+    got = model_io.dump_scans(paths["left"], paths["right"], dst)
+    assert got.shape == g["axangles"].shape == (73, 15, 3)
+    assert np.array_equal(got, g["axangles"])
+    assert np.array_equal(np.load(dst, allow_pickle=False), g["axangles"])
+    pose = model_io.scans_to_pose(got)                  # data_explore.py:13
+    assert pose.shape == (73, 16, 3) and np.all(pose[:, 0] == 0) and np.array_equal(pose[:, 1:], got)
