@@ -141,8 +141,9 @@ def cpu_baseline(procs, seconds):
                       f"processes x {ph['seconds']:.1f} s, OMP_NUM_THREADS=1; "
                       "beta ~ N(0,1), pose ~ N(0,0.5^2)",
             "batched": {"value": bt["value"], "unit": "hands/s", "cores": procs,
-                        "sample": f"{bt['hands']} hands in 256-hand float64 einsum batches "
-                                  f"(oracle.forward) in {procs} processes x {bt['seconds']:.1f} s"}}
+                        "sample": f"{bt['hands']} hands in 256-hand float64 BLAS-GEMM batches "
+                                  f"(oracle/cpu_baseline.py forward_gemm) in {procs} processes x "
+                                  f"{bt['seconds']:.1f} s, OMP_NUM_THREADS=1"}}
 
 
 def load_traffic(path, kernel, batch):

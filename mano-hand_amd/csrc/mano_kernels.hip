@@ -3,7 +3,8 @@
 // Reference hot path: MANOModel.update() in /root/reference/mano_np.py:79-115.
 // mano_forward is two launches on the caller's stream:
 //
-//   articulate    one lane per (hand, joint), 32 hands per 512-thread block:
+//   articulate    one lane per (hand, joint), 16 hands per 256-thread block
+//                 (optionally the PCA pose map of set_params, :66-72, first):
 //                 Rodrigues (mano_np.py:117-148) in sinc / half-angle form,
 //                 rest joints J = Jreg.T + (Jreg.S).beta (:83, folded in float64
 //                 at model load), the 16-joint chain (:96-104) as 3 dependent
@@ -188,9 +189,9 @@ __device__ __forceinline__ void pca_joint_pose(const PcaInput& in, const float* 
   }
 }
 
-// kPca: the pose comes from PCA coefficients (pca_joint_pose prologue, the
+// kFromPca: the pose comes from PCA coefficients (pca_joint_pose prologue, the
 // basis rows in use staged in LDS) instead of the axis-angle `pose` input.
-template <bool kPca>
+template <bool kFromPca>
 __global__ __launch_bounds__(256) void articulate_kernel(
     const float* __restrict__ betas, int64_t betas_stride, const float* __restrict__ pose,
     const float* __restrict__ trans, const float* __restrict__ joint_template,
@@ -210,7 +211,7 @@ __global__ __launch_bounds__(256) void articulate_kernel(
   if (tid < kJoints * 3) jt_s[tid] = joint_template[tid];
   const float* basis_s = nullptr;
   const float* mean_s = nullptr;
-  if constexpr (kPca) {
+  if constexpr (kFromPca) {
     __shared__ float pb_s[kPca * kPca + kPca];
     for (int i = tid; i < pca.n_comps * kPca; i += 256) pb_s[i] = pca_basis[i];
     if (tid < kPca) pb_s[kPca * kPca + tid] = pca_mean[tid];
@@ -225,7 +226,7 @@ __global__ __launch_bounds__(256) void articulate_kernel(
   const bool valid = h0 + hl < n;
 
   float aa[3];
-  if constexpr (kPca) {
+  if constexpr (kFromPca) {
     pca_joint_pose(pca, basis_s, mean_s, h, j, aa);
     if (valid && pca.pose_out) {
 #pragma unroll
