@@ -44,8 +44,26 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 // An opaque scalar: the value leaves the vectorizer's reach (no packed fp32).
+// MANO_H3_NO_PACK=0 (debug builds for tools/debug/h3_root_cause.sh only)
+// makes it transparent again.
+#ifndef MANO_H3_NO_PACK
+#define MANO_H3_NO_PACK 1
+#endif
 __device__ __forceinline__ float no_pack(float x) {
+#if MANO_H3_NO_PACK
   asm("" : "+v"(x));
+#endif
+  return x;
+}
+// MANO_H3_SCALAR_UNSCALE=1 (debug builds): the LBS output's final
+// fma(o, 2^-k, trans) stays scalar even when no_pack is transparent.
+#ifndef MANO_H3_SCALAR_UNSCALE
+#define MANO_H3_SCALAR_UNSCALE 0
+#endif
+__device__ __forceinline__ float no_pack_unscale(float x) {
+#if MANO_H3_NO_PACK || MANO_H3_SCALAR_UNSCALE
+  asm("" : "+v"(x));
+#endif
   return x;
 }
 
@@ -171,7 +189,7 @@ __device__ __forceinline__ void lbs_h3(const f16x8 (&F)[12], const f16x8& w1, co
       float o = T[c * 4 + 3][r];
 #pragma unroll
       for (int k = 2; k >= 0; --k) o = no_pack(fmaf(T[c * 4 + k][r], p[k][r], o));
-      out[c][r] = no_pack(fmaf(o, t_unscale, tr[r][c]));
+      out[c][r] = no_pack_unscale(fmaf(o, t_unscale, tr[r][c]));
     }
 }
 
@@ -184,9 +202,13 @@ __device__ __forceinline__ void lbs_h3(const f16x8 (&F)[12], const f16x8& w1, co
 // count together, in issue order) and every LDS access.  __syncthreads() would
 // add the workgroup release fence, i.e. vmcnt(0): a wait on the group's output
 // stores that the LDS hand-off does not need.
+// MANO_H3_FULL_WAIT=1 (debug builds) waits for every vector-memory op instead.
+#ifndef MANO_H3_FULL_WAIT
+#define MANO_H3_FULL_WAIT 0
+#endif
 template <int N>
 __device__ __forceinline__ void barrier_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(MANO_H3_FULL_WAIT ? 0 : N) : "memory");
 }
 
 __device__ __forceinline__ void unit_range_h3(int64_t units, int64_t worker, int64_t n_workers,
