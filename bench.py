@@ -59,13 +59,13 @@ PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, s
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 WORKLOADS = {
-    "C2": {"hands": 65536, "trans": False, "gather": False, "seed": 1002,
+    "C2": {"hands": 65536, "trans": False, "gather": False, "seed": 1001,
            "desc": "C2: full-pose fp32 MANO forward, 65,536 hands per GPU, verts + joints"},
-    "C3": {"hands": 2097152, "trans": False, "gather": False, "seed": 1003,
+    "C3": {"hands": 2097152, "trans": False, "gather": False, "seed": 1002,
            "desc": "C3: 2,097,152 hands per GPU (16M over 8 GPUs), per-shard verts + joints"},
-    "C4": {"hands": 524288, "trans": False, "gather": True, "seed": 1004,
+    "C4": {"hands": 524288, "trans": False, "gather": True, "seed": 1003,
            "desc": "C4: 524,288 hands per GPU (4M over 8 GPUs), RCCL gather of verts + joints to GPU 0"},
-    "C5": {"hands": 1048576, "trans": True, "gather": False, "seed": 1005,
+    "C5": {"hands": 1048576, "trans": True, "gather": False, "seed": 1004,
            "desc": "C5: 1,048,576 hands per GPU, per-hand betas + global rot + trans, verts + joints"},
 }
 

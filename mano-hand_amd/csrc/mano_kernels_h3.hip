@@ -22,12 +22,14 @@
 //
 // Packed fp32 VALU (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32) is kept out of
 // these kernels: every scalar result the vectorizer could pair goes through
-// no_pack(), and the library is built with -fno-slp-vectorize.  With packed
-// ops in the LBS apply, blend_skin_h3 returned wrong coordinate-0 values in
-// lanes 48-63 (rows 12-15 of a tile) in a timing-dependent subset of groups;
-// the disassembly had a v_pk_fma_f32 immediately followed by a VALU write of
-// one of its source registers.  Packed fp32 beside MFMA is also the slower
-// form on gfx950 (MI355X_MICROARCH.md), so nothing is lost.
+// no_pack(), and the library is built with -fno-slp-vectorize.  With the
+// vectorizer on, blend_skin_h3's rest_verts instantiations returned wrong x
+// coordinates for hand rows 14-15 under load; round 2 localized it to the
+// v_pk_fma_f32 with an SGPR-pair multiplier made of the final
+// fma(o, 2^-k, trans) -- scalarizing only that multiply removes every failure
+// -- and excluded wait-state hazards, the counted vmcnt barriers, stray
+// stores and spills (tools/debug/h3_root_cause.sh).  Packed
+// fp32 beside MFMA is also the slower form on gfx950 (MI355X_MICROARCH.md).
 #include "mano_internal.h"
 #include "mano_span.h"
 
