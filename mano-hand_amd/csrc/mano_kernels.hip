@@ -521,6 +521,15 @@ __device__ __forceinline__ void prio_down() {
 #ifndef MANO_BS_STORE_PRIO
 #define MANO_BS_STORE_PRIO 0  // blend_skin16: priority while issuing the point stores
 #endif
+// Diagnostic builds only (tools/debug/bs_ablate.sh): 1 = no output stores
+// (a never-taken data-dependent store keeps the work alive), 2 = no LBS
+// (v_posed is stored as verts), 3 = both, 4 = the same stores into a
+// line-aligned scratch layout (each 192-B hand segment at a 256-B boundary:
+// same instructions and bytes, no partially written lines; the verts buffer
+// must hold n * n_groups * 256 B).
+#ifndef MANO_BS_ABLATE
+#define MANO_BS_ABLATE 0
+#endif
 
 // Fused blend GEMM + LBS.  A block owns a contiguous range of (quad of 4
 // hand tiles, vertex group) units; at each quad its waves load their A
@@ -540,7 +549,7 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
   // One slot: a basis tile (10 KB) + the group's W fragment (1 KB, with the
   // group's first tile); ring of 3.
   constexpr int kRingF4 = (kGroups16 + 1) * 64;
-  constexpr int kStores = kVposed ? 8 : 4;   // global_store_dwordx3 per group
+  constexpr int kStores = (MANO_BS_ABLATE & 1) ? 0 : kVposed ? 8 : 4;  // global_store_dwordx3 per group
   // vmcnt of the barrier after tile t: the wave's memory ops issued after tile
   // t + 1's DMA -- tile t + 2's DMA (at least 2 pieces per wave) and, after a
   // group's first tile, the previous group's stores.
@@ -644,7 +653,18 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
       if (vb > n_verts - 16) vb = n_verts - 16;
       const int voff = 3 * (vb + col);
       f32x4 out[3];
-      lbs_apply16(F, wf, p, out);
+      if constexpr (MANO_BS_ABLATE & 2) {
+        out[0] = p[0];
+        out[1] = p[1];
+        out[2] = p[2];
+        (void)wf;
+      } else {
+        lbs_apply16(F, wf, p, out);
+      }
+      if constexpr (MANO_BS_ABLATE & 1) {
+        if (out[0][0] == 1234.5f && out[1][1] == 2345.5f) vtile[voff] = out[2][2];
+        continue;
+      }
       prio_up<kStorePrio>();
       // One 12-B point store per row; rows past the batch end rewrite the
       // last hand's identical values.
@@ -657,7 +677,10 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
           o1 += trs[wave][hr * 3 + 1];
           o2 += trs[wave][hr * 3 + 2];
         }
-        *reinterpret_cast<f32x3*>(vtile + unsigned(hr * vstride32 + voff)) = f32x3{o0, o1, o2};
+        if constexpr (MANO_BS_ABLATE == 4)  // needs a verts buffer of n * 49 * 256 B
+          *reinterpret_cast<f32x3*>(verts + ((h0 + hr) * n_groups + grp) * 64 + 3 * col) = f32x3{o0, o1, o2};
+        else
+          *reinterpret_cast<f32x3*>(vtile + unsigned(hr * vstride32 + voff)) = f32x3{o0, o1, o2};
         if constexpr (kVposed)
           *reinterpret_cast<f32x3*>(ptile + unsigned(hr * vstride32 + voff)) = f32x3{p[0][r], p[1][r], p[2][r]};
       }

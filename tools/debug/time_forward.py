@@ -17,7 +17,7 @@ pose = 0.5 * torch.randn((B, 16, 3), generator=g, device=dev)
 ref = None
 for prec in ("fp32", "f16x3"):
     m = ManoHip(synthetic_params(0), device=0, precision=prec)
-    v = torch.empty((B, 778, 3), device=dev)
+    v = torch.empty((B, int(os.environ.get("VERTS_ROW", 778)), 3), device=dev)
     m.stage_articulate(betas, pose)
     for _ in range(300):
         m.stage_blend_skin(B, v)
@@ -35,7 +35,7 @@ for prec in ("fp32", "f16x3"):
     ms_art = float(np.mean([a.elapsed_time(b) for a, b in ev2]))
     if ref is None:
         ref = v.clone()
-    err = (v - ref).abs().max().item()
+    err = (v[:, :778] - ref[:, :778]).abs().max().item()
     print(f"{os.path.basename(_abi.LIB_PATH):24s} {prec:6s} blend_skin {ms:.4f} ms  articulate {ms_art:.4f} ms  "
           f"vs fp32 max {err:.2e}", flush=True)
     m.close()
