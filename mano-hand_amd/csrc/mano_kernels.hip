@@ -21,6 +21,8 @@
 // v_mfma_f32_32x32x2_f32, v_posed to HBM) and skin_span (HBM-streaming LBS
 // with the same MFMA transform tiles as blend_skin16, so both paths agree bit
 // for bit).
+#include <algorithm>
+
 #include "mano_internal.h"
 #include "mano_span.h"
 
@@ -751,6 +753,186 @@ __global__ __launch_bounds__(256, MANO_SPAN_BLOCKS_PER_CU) void skin_span_kernel
                   int(threadIdx.x & 63));
 }
 
+#ifndef MANO_SKIN_RING
+#define MANO_SKIN_RING 0  // standalone LBS: skin_span (default) or skin_ring (split roles)
+#endif
+#if MANO_SKIN_RING
+// ---------------------------------------------------------------------------
+// skin_ring: the standalone LBS (mano_np.py:112-115) with split roles.  One
+// 8-wave block per CU: waves 0-3 compute, waves 4-7 load; pair w = (compute
+// wave w, load wave w + 4) shares a SIMD.  Full 64-vertex spans (units of 16
+// hands x 64 vertices, as skin_span) flow through three LDS slots per pair
+// in lock-step phases:
+//   phase p   load wave: LDS-DMA of unit(p) into slot p % 3, one 768-B row per
+//             global_load_lds_dwordx4 on 48 lanes (padded row stride, so the
+//             D-layout point reads are conflict-free); two units per pair stay
+//             in flight (the barrier waits only for unit(p - 1));
+//             compute wave: skins unit(p - 2) from slot (p - 2) % 3 with
+//             blend_skin16's MFMA transform tiles and fmaf order (bit-exact
+//             with the fused kernel) and stores the points straight from
+//             registers (12-B rows, as blend_skin16); its operands (transform
+//             fragments, weights, trans) are fetched one phase ahead;
+//   one workgroup barrier (load: unit(p - 1) landed -- counted vmcnt;
+//   compute: its slot reads done).
+// The compute wave never waits on HBM loads and the load wave never on the
+// MFMA pipe.  Units go to pairs in grid-stride order (XCD-aware pair ids), so
+// the chip streams a compact window.  The n_verts % 64 tail of each tile runs
+// after the ring on the compute waves through the per-group point path.
+// ---------------------------------------------------------------------------
+constexpr int kRingPairs = 4;
+constexpr int kRingSlots = 3;
+constexpr int kRingLdsBytes = kRingSlots * kRingPairs * span::kStageFloats * 4;  // 150,528 B
+constexpr int kRingRowLanes = 3 * span::kVerts / 4;  // 48 lanes x 16 B = one 768-B span row
+
+// One LDS-DMA row: lanes 0..47 each move 16 B (global_load_lds_dwordx4) from
+// their source into lds_dst + 16 x lane.  (global_load_lds_dwordx3 writes lane
+// l at lds_dst + 16 l as well, not 12 l -- tools/microbench/lds_dma_x3.hip --
+// and the x4 form reads 4-B-aligned sources correctly.)  The load wave reads
+// no LDS itself, so hipcc's view of the DMA as a pending LDS write costs
+// nothing; the phase barrier's counted vmcnt orders it for the readers.
+__device__ __forceinline__ void dma_row(const float* gsrc, float* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+
+template <bool kTrans>
+__global__ __launch_bounds__(512, 1) void skin_ring_kernel(
+    const float* __restrict__ transforms, const float* __restrict__ wfrag16,
+    const float* __restrict__ vposed, const float* __restrict__ trans, float* __restrict__ verts,
+    int64_t n, int n_verts, int n_groups) {
+  extern __shared__ float ring_lds[];
+  using Lbs = SpanLbs16<kTrans>;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int w = wave & (kRingPairs - 1);
+  const bool is_load = wave >= kRingPairs;
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+v"(lane));
+  const int vstride = 3 * n_verts;
+  const int n_full = n_verts / span::kVerts;
+  const int n_tail = n_groups - span::kGroups * n_full;
+  const int64_t nt16 = (n + 15) / 16;
+  const int64_t units = nt16 * n_full;
+  const int64_t b = blockIdx.x, nb = gridDim.x;
+  const int64_t blk = (nb % 8) ? b : (b % 8) * (nb / 8) + b / 8;  // XCD-aware (L2 locality only)
+  const int64_t pair = blk * kRingPairs + w;
+  const int64_t n_pairs = nb * kRingPairs;
+  const int64_t n_phases = (units + n_pairs - 1) / n_pairs;
+  const int row0 = 4 * (lane >> 4), col = lane & 15;
+  auto slot = [&](int64_t p) {
+    return ring_lds + (int(p % kRingSlots) * kRingPairs + w) * span::kStageFloats;
+  };
+  auto unit_ok = [&](int64_t p) { return p >= 0 && p < n_phases && p * n_pairs + pair < units; };
+  auto rows_of = [&](int64_t t) {
+    const int64_t left = n - 16 * t;
+    return int(left < 16 ? left : 16);
+  };
+
+  // The two roles run separate loops with the same barrier count, so the
+  // compiler's wait analysis of one never leaks into the other (a merged loop
+  // made the load wave wait vmcnt(0) on the compute wave's operand copies).
+  if (is_load) {
+    for (int64_t p = 0; p < n_phases + 2; ++p) {
+      if (unit_ok(p)) {
+        const int64_t u = p * n_pairs + pair;
+        const int64_t t = u / n_full;
+        const int sp = int(u - t * n_full);
+        const int n_valid = rows_of(t);
+        const float* src = vposed + 16 * t * int64_t(vstride) + 3 * span::kVerts * sp + 4 * lane;
+        float* dst = slot(p);
+        if (lane < kRingRowLanes) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int rr = r < n_valid ? r : n_valid - 1;  // rows past the batch end repeat the last hand
+            dma_row(src + unsigned(rr * vstride), dst + r * span::kStride);
+          }
+        }
+        // unit(p - 1) has landed; unit(p)'s 16 rows stay in flight
+        asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      }
+    }
+    return;
+  }
+
+  // Compute waves: two operand sets in ping-pong (unit(q) is skinned at phase
+  // q + 2 with set a for even q, b for odd q, its operands loaded one phase
+  // earlier), so no register copy -- and no wait for this wave's in-flight
+  // stores -- sits between the phases.
+  Lbs lbs_a{transforms, wfrag16, trans, {}}, lbs_b{transforms, wfrag16, trans, {}};
+  f32x4 w_a[span::kGroups], w_b[span::kGroups];
+  auto prefetch = [&](int64_t p, Lbs& into, f32x4 (&w_into)[span::kGroups]) {  // operands of unit(p)
+    const int64_t u = p * n_pairs + pair;
+    const int64_t t = u / n_full;
+    const int sp = int(u - t * n_full);
+    into.fetch_tile(16 * t, n, rows_of(t), lane, into.cur);
+#pragma unroll
+    for (int g = 0; g < span::kGroups; ++g) w_into[g] = into.load_w(span::kGroups * sp + g, lane);
+  };
+  auto step = [&](int64_t p, Lbs& use, f32x4 (&w_use)[span::kGroups], Lbs& pf,
+                  f32x4 (&w_pf)[span::kGroups]) {
+    if (p >= n_phases + 2) return;
+    if (unit_ok(p - 2)) {  // unit(p - 1) is then the next one, if any
+      const int64_t u = (p - 2) * n_pairs + pair;
+      const int64_t t = u / n_full;
+      const int sp = int(u - t * n_full);
+      const int n_valid = rows_of(t);
+      if (unit_ok(p - 1)) prefetch(p - 1, pf, w_pf);
+      const float* st = slot(p - 2);
+      float* dst = verts + 16 * t * int64_t(vstride) + 3 * span::kVerts * sp;
+#pragma unroll
+      for (int g = 0; g < span::kGroups; ++g) {
+        float pts[4][3], o[4][3];
+        span::read_points(st, lane, g, pts);
+        use.apply(w_use[g], pts, o);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const unsigned off = unsigned(min(row0 + r, n_valid - 1) * vstride + 3 * (16 * g + col));
+          *reinterpret_cast<f32x3*>(dst + off) = f32x3{o[r][0], o[r][1], o[r][2]};
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one group's LBS temporaries live at a time
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+  if (unit_ok(0)) prefetch(0, lbs_a, w_a);
+  for (int64_t p = 0; p < n_phases + 2; p += 2) {
+    step(p, lbs_a, w_a, lbs_b, w_b);
+    step(p + 1, lbs_b, w_b, lbs_a, w_a);
+  }
+  Lbs& lbs = lbs_a;
+  if (n_tail == 0) return;
+
+  // The tail groups of every tile (vertices past the last full span), on the
+  // compute waves: points straight from HBM, the last group shifted to end at
+  // n_verts (skin_span's tail path).
+  for (int64_t t = pair; t < nt16; t += n_pairs) {
+    const int n_valid = rows_of(t);
+    lbs.fetch_tile(16 * t, n, n_valid, lane, lbs.cur);
+    const float* src = vposed + 16 * t * int64_t(vstride);
+    float* dst = verts + 16 * t * int64_t(vstride);
+    for (int g = 0; g < n_tail; ++g) {
+      const int vb = min(16 * (span::kGroups * n_full + g), n_verts - 16);
+      const f32x4 wg = lbs.load_w(span::kGroups * n_full + g, lane);
+      float pts[4][3], o[4][3];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const unsigned off = unsigned(min(row0 + r, n_valid - 1) * vstride + 3 * (vb + col));
+        const f32x3 v = *reinterpret_cast<const f32x3*>(src + off);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) pts[r][c] = v[c];
+      }
+      lbs.apply(wg, pts, o);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const unsigned off = unsigned(min(row0 + r, n_valid - 1) * vstride + 3 * (vb + col));
+        *reinterpret_cast<f32x3*>(dst + off) = f32x3{o[r][0], o[r][1], o[r][2]};
+      }
+    }
+  }
+}
+#endif  // MANO_SKIN_RING
+
 // ---------------------------------------------------------------------------
 // PCA pose (mano_np.py:66-72) and standalone Rodrigues (:117-148).
 // ---------------------------------------------------------------------------
@@ -943,6 +1125,31 @@ hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* featu
 hipError_t launch_skin(const DeviceModel& m, int64_t n, const float* transforms,
                        const float* vposed, const float* trans, float* verts,
                        hipStream_t stream) {
+#if MANO_SKIN_RING
+  {
+    // 147 KB of dynamic LDS per block: raise the function's limit once.
+    static hipError_t attr = [] {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(skin_ring_kernel<true>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, kRingLdsBytes);
+      if (e == hipSuccess)
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(skin_ring_kernel<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kRingLdsBytes);
+      return e;
+    }();
+    if (attr != hipSuccess) return attr;
+    const int64_t nt16 = (n + 15) / 16;
+    const int64_t units = nt16 * (m.n_verts / span::kVerts);
+    int64_t blocks = std::max((units + kRingPairs - 1) / kRingPairs, (nt16 + kRingPairs - 1) / kRingPairs);
+    blocks = std::min<int64_t>(blocks, m.n_cu > 0 ? m.n_cu : 1);
+    auto launch = [&](auto kernel) {
+      hipLaunchKernelGGL(kernel, dim3(unsigned(blocks)), dim3(64 * 2 * kRingPairs), kRingLdsBytes, stream,
+                         transforms, m.wfrag16, vposed, trans, verts, n, m.n_verts, m.n_groups16);
+    };
+    if (trans) launch(skin_ring_kernel<true>);
+    else launch(skin_ring_kernel<false>);
+    return hipGetLastError();
+  }
+#endif
   const int64_t units = (n + 15) / 16 * span::n_spans(m.n_verts);
   auto launch = [&](auto kernel) {
     hipLaunchKernelGGL(kernel, persistent_grid(kernel, m, units, 4, kSkinBlocksPerCU), dim3(256), 0,

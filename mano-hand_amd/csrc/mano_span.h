@@ -69,7 +69,10 @@ __device__ __forceinline__ void sweep_slot(int i, int lane, int& row, int& c4) {
 }
 
 // The 16 rows of a span, HBM -> registers (rows past the batch end re-read
-// the tile's last hand).
+// the tile's last hand).  MANO_SPAN_NT_LOAD: non-temporal (read-once) loads.
+#ifndef MANO_SPAN_NT_LOAD
+#define MANO_SPAN_NT_LOAD 0
+#endif
 __device__ __forceinline__ void load_rows(const float* __restrict__ tile, int vstride, int v0,
                                           int n_valid, int lane, f32x4u (&buf)[kF4]) {
 #pragma unroll
@@ -77,7 +80,9 @@ __device__ __forceinline__ void load_rows(const float* __restrict__ tile, int vs
     int row, c4;
     sweep_slot(i, lane, row, c4);
     const unsigned off = unsigned(min(row, n_valid - 1) * vstride + 4 * c4);
-    buf[i] = *reinterpret_cast<const f32x4u*>(tile + 3 * v0 + off);
+    const f32x4u* src = reinterpret_cast<const f32x4u*>(tile + 3 * v0 + off);
+    if constexpr (MANO_SPAN_NT_LOAD) buf[i] = __builtin_nontemporal_load(src);
+    else buf[i] = *src;
   }
 }
 

@@ -15,7 +15,7 @@ from collections import defaultdict
 
 # demangled-name prefix -> bench.py kernel key
 KERNELS = {"blend_skin16_kernel<": "blend_skin", "blend_kernel(": "blend", "skin_span_kernel<": "skin",
-           "articulate_kernel(": "articulate", "blend_skin_h3_kernel<": "blend_skin_h3",
+           "articulate_kernel<": "articulate", "blend_skin_h3_kernel<": "blend_skin_h3",
            "skin_span_h3_kernel<": "skin_h3"}
 # FETCH_SIZE correction (MI355X_MICROARCH.md §HBM): on gfx950 the counter
 # reports half the bytes of wide coalesced streams.  Measured here it is x2 for
@@ -32,14 +32,14 @@ def short(name):
     return None
 
 
-def main(d):
+def main(d, batch=65536):
     acc = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> per-dispatch values
     for f in glob.glob(os.path.join(d, "*", "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
             k = short(r["Kernel_Name"])
             if k is not None:
                 acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    out = {"batch": 65536, "kernels": {}}
+    out = {"batch": batch, "kernels": {}}
     for k, cs in sorted(acc.items()):
         avg = {c: sum(v) / len(v) for c, v in cs.items()}
         print(f"{k:12s}")
@@ -57,4 +57,4 @@ def main(d):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 65536)
