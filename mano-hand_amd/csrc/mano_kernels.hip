@@ -308,6 +308,9 @@ __device__ __forceinline__ f32x16 mfma_tile(const float (&a)[kKGroups * 4], cons
   return acc;
 }
 
+#ifndef MANO_BLEND_NT_STORE
+#define MANO_BLEND_NT_STORE 0  // nontemporal v_posed stores in the unfused blend GEMM
+#endif
 __device__ __forceinline__ void store_vposed_tile(float* __restrict__ vposed, const f32x16& acc,
                                                   int64_t h0, int col, int64_t n, int n_cols,
                                                   int hi) {
@@ -316,7 +319,10 @@ __device__ __forceinline__ void store_vposed_tile(float* __restrict__ vposed, co
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int64_t h = h0 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-      if (h < n) vposed[h * n_cols + col] = acc[r];
+      if (h < n) {
+        if constexpr (MANO_BLEND_NT_STORE) __builtin_nontemporal_store(acc[r], vposed + h * n_cols + col);
+        else vposed[h * n_cols + col] = acc[r];
+      }
     }
   }
 }
@@ -387,11 +393,17 @@ __global__ __launch_bounds__(256, 2) void blend_kernel(
 // each other's barrier / LDS / store stalls.
 // ---------------------------------------------------------------------------
 typedef float f32x4v __attribute__((ext_vector_type(4)));
+#ifndef MANO_BS_SPLIT
+#define MANO_BS_SPLIT 0  // experiment: two interleaved accumulators per GEMM tile chain
+#endif
 
 __device__ __forceinline__ f32x4 mfma16_tile(const float (&a)[kGroups16 * 4],
                                              const f32x4* __restrict__ b, int lane) {
   f32x4 acc = {};
   f32x4 bn = b[lane];
+#if MANO_BS_SPLIT
+  f32x4 acc1 = {};
+#endif
 #pragma unroll
   for (int g = 0; g < kGroups16; ++g) {
     const f32x4 bv = bn;
@@ -399,8 +411,18 @@ __device__ __forceinline__ f32x4 mfma16_tile(const float (&a)[kGroups16 * 4],
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
+#if MANO_BS_SPLIT
+      if (4 * g + q < kSteps16) {
+        if (q & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[4 * g + q], bv[q], acc1, 0, 0, 0);
+        else acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[4 * g + q], bv[q], acc, 0, 0, 0);
+      }
+#else
       if (4 * g + q < kSteps16) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[4 * g + q], bv[q], acc, 0, 0, 0);
+#endif
   }
+#if MANO_BS_SPLIT
+  acc += acc1;
+#endif
   return acc;
 }
 
@@ -532,6 +554,32 @@ __device__ __forceinline__ void prio_down() {
 #ifndef MANO_BS_ABLATE
 #define MANO_BS_ABLATE 0
 #endif
+// 8 = barriers without s_barrier (waits only; results wrong), 16 = no basis
+// DMA after the prologue (results wrong).
+template <int N>
+__device__ __forceinline__ void bs_barrier() {
+#if MANO_BS_ABLATE & 8
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+#else
+  barrier_vmcnt<N>();
+#endif
+}
+// blend_skin16's verts point stores are nontemporal when verts is the only
+// output stream (same-box A/B at 65,536 hands, tools/debug/time_stages.py:
+// 0.493 vs 0.504 ms, identical bits).  With rest_verts as a second stream
+// they are plain: nontemporal there took 0.85 vs 0.61 ms, and the unfused
+// blend GEMM (0.60 vs 0.37) and blend_skin_h3 (0.40 vs 0.26) lose the same way.
+#ifndef MANO_BS_NT_STORE
+#define MANO_BS_NT_STORE 1
+#endif
+template <bool kNt>
+__device__ __forceinline__ void store_out(float* dst, f32x3 v) {
+  if constexpr (kNt) __builtin_nontemporal_store(v, reinterpret_cast<f32x3*>(dst));
+  else *reinterpret_cast<f32x3*>(dst) = v;
+}
+#ifndef MANO_BS_SLOTS
+#define MANO_BS_SLOTS 3  // blend_skin16 basis ring: 3 slots (DMA 2 tiles ahead) or 4 (3 ahead)
+#endif
 
 // Fused blend GEMM + LBS.  A block owns a contiguous range of (quad of 4
 // hand tiles, vertex group) units; at each quad its waves load their A
@@ -551,13 +599,14 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
   // One slot: a basis tile (10 KB) + the group's W fragment (1 KB, with the
   // group's first tile); ring of 3.
   constexpr int kRingF4 = (kGroups16 + 1) * 64;
+  constexpr int kSlots = MANO_BS_SLOTS;
   constexpr int kStores = (MANO_BS_ABLATE & 1) ? 0 : kVposed ? 8 : 4;  // global_store_dwordx3 per group
   // vmcnt of the barrier after tile t: the wave's memory ops issued after tile
   // t + 1's DMA -- tile t + 2's DMA (at least 2 pieces per wave) and, after a
   // group's first tile, the previous group's stores.
   constexpr int kPieces = kGroups16 / 4;     // LDS-DMA pieces per wave and tile, at least
   constexpr int kDmaPrio = MANO_BS_DMA_PRIO, kStorePrio = MANO_BS_STORE_PRIO;
-  __shared__ f32x4 lds[3 * kRingF4];
+  __shared__ f32x4 lds[kSlots * kRingF4];
   __shared__ float trs[4][16 * 3];  // the wave's 16 translations, read back at the stores
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int vstride32 = 3 * n_verts;
@@ -618,39 +667,86 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
                                          16, 0, 0);
       }
     };
+#if MANO_BS_SLOTS == 4
+    // Ring of 4 slots, tile t in slot t & 3, DMA three tiles ahead: a group's
+    // stores are followed by two tile DMAs before a barrier waits on a DMA
+    // issued after them (vmcnt retires in issue order), so the stores get two
+    // tile times to drain instead of one.
+    auto slot = [&](int t) { return lds + (t & 3) * kRingF4; };
+    stage_basis_tile16(basis16, 3 * g0, slot(3 * g0), wave, lane);
+    stage_w(g0, slot(3 * g0));
+    stage_basis_tile16(basis16, 3 * g0 + 1, slot(3 * g0 + 1), wave, lane);
+    stage_basis_tile16(basis16, 3 * g0 + 2, slot(3 * g0 + 2), wave, lane);
+    bs_barrier<0>();
+    for (int grp = g0; grp < g1; ++grp) {
+      const bool more = grp + 1 < g1;
+      const int t0 = 3 * grp;
+      f32x4 p[3];
+      // Barrier after tile t waits for tile t + 1's DMA.  Younger ops then:
+      // q = 0, 1 -- two tiles' DMA and the previous group's stores; q = 2 --
+      // two tiles' DMA.  Last group of the range (no DMA ahead): q = 0 --
+      // one tile's DMA + the stores, q = 1, 2 -- the stores.
+      const f32x4 wf = slot(t0)[kGroups16 * 64 + lane];
+      if (more) {
+        prio_up<kDmaPrio>();
+        if constexpr (!(MANO_BS_ABLATE & 16)) stage_basis_tile16(basis16, t0 + 3, slot(t0 + 3), wave, lane);
+        stage_w(grp + 1, slot(t0 + 3));
+        prio_down<kDmaPrio>();
+      }
+      p[0] = mfma16_tile(a, slot(t0), lane);
+      if (more) bs_barrier<2 * kPieces + kStores>();
+      else bs_barrier<kPieces + kStores>();
+      if (more) {
+        prio_up<kDmaPrio>();
+        if constexpr (!(MANO_BS_ABLATE & 16)) stage_basis_tile16(basis16, t0 + 4, slot(t0 + 4), wave, lane);
+        prio_down<kDmaPrio>();
+      }
+      p[1] = mfma16_tile(a, slot(t0 + 1), lane);
+      if (more) bs_barrier<2 * kPieces + kStores>();
+      else bs_barrier<kStores>();
+      if (more) {
+        prio_up<kDmaPrio>();
+        if constexpr (!(MANO_BS_ABLATE & 16)) stage_basis_tile16(basis16, t0 + 5, slot(t0 + 5), wave, lane);
+        prio_down<kDmaPrio>();
+      }
+      p[2] = mfma16_tile(a, slot(t0 + 2), lane);
+      if (more) bs_barrier<2 * kPieces>();
+      else bs_barrier<kStores>();
+#else
     stage_basis_tile16(basis16, 3 * g0, lds, wave, lane);
     stage_w(g0, lds);
     stage_basis_tile16(basis16, 3 * g0 + 1, lds + kRingF4, wave, lane);
-    barrier_vmcnt<0>();  // the first two tiles and every prologue load have landed
+    bs_barrier<0>();  // the first two tiles and every prologue load have landed
 
     for (int grp = g0; grp < g1; ++grp) {
       const bool more = grp + 1 < g1;
       f32x4 p[3];
       // Tile 3 grp + q in slot q; tile 3 grp + q + 2 goes to slot (q + 2) % 3.
       prio_up<kDmaPrio>();
-      stage_basis_tile16(basis16, 3 * grp + 2, lds + 2 * kRingF4, wave, lane);
+      if constexpr (!(MANO_BS_ABLATE & 16)) stage_basis_tile16(basis16, 3 * grp + 2, lds + 2 * kRingF4, wave, lane);
       prio_down<kDmaPrio>();
       const f32x4 wf = lds[kGroups16 * 64 + lane];  // read before slot 0 is re-staged
       p[0] = mfma16_tile(a, lds, lane);
-      if (grp == g0) barrier_vmcnt<kPieces>();
-      else barrier_vmcnt<kPieces + kStores>();
+      if (grp == g0) bs_barrier<kPieces>();
+      else bs_barrier<kPieces + kStores>();
       if (more) {
         prio_up<kDmaPrio>();
-        stage_basis_tile16(basis16, 3 * grp + 3, lds, wave, lane);
+        if constexpr (!(MANO_BS_ABLATE & 16)) stage_basis_tile16(basis16, 3 * grp + 3, lds, wave, lane);
         stage_w(grp + 1, lds);
         prio_down<kDmaPrio>();
       }
       p[1] = mfma16_tile(a, lds + kRingF4, lane);
-      if (more) barrier_vmcnt<kPieces>();
-      else barrier_vmcnt<0>();
+      if (more) bs_barrier<kPieces>();
+      else bs_barrier<0>();
       if (more) {
         prio_up<kDmaPrio>();
-        stage_basis_tile16(basis16, 3 * grp + 4, lds + kRingF4, wave, lane);
+        if constexpr (!(MANO_BS_ABLATE & 16)) stage_basis_tile16(basis16, 3 * grp + 4, lds + kRingF4, wave, lane);
         prio_down<kDmaPrio>();
       }
       p[2] = mfma16_tile(a, lds + 2 * kRingF4, lane);
-      if (more) barrier_vmcnt<kPieces>();
-      else barrier_vmcnt<0>();
+      if (more) bs_barrier<kPieces>();
+      else bs_barrier<0>();
+#endif
       int vb = grp * 16;
       if (vb > n_verts - 16) vb = n_verts - 16;
       const int voff = 3 * (vb + col);
@@ -682,9 +778,9 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
         if constexpr (MANO_BS_ABLATE == 4)  // needs a verts buffer of n * 49 * 256 B
           *reinterpret_cast<f32x3*>(verts + ((h0 + hr) * n_groups + grp) * 64 + 3 * col) = f32x3{o0, o1, o2};
         else
-          *reinterpret_cast<f32x3*>(vtile + unsigned(hr * vstride32 + voff)) = f32x3{o0, o1, o2};
+          store_out<MANO_BS_NT_STORE && !kVposed>(vtile + unsigned(hr * vstride32 + voff), f32x3{o0, o1, o2});
         if constexpr (kVposed)
-          *reinterpret_cast<f32x3*>(ptile + unsigned(hr * vstride32 + voff)) = f32x3{p[0][r], p[1][r], p[2][r]};
+          store_out<false>(ptile + unsigned(hr * vstride32 + voff), f32x3{p[0][r], p[1][r], p[2][r]});
       }
       prio_down<kStorePrio>();
     }

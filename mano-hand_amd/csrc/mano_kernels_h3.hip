@@ -213,6 +213,14 @@ __device__ __forceinline__ void barrier_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(MANO_H3_FULL_WAIT ? 0 : N) : "memory");
 }
 
+#ifndef MANO_H3_NT_STORE
+#define MANO_H3_NT_STORE 0  // nontemporal output point stores (as blend_skin16's)
+#endif
+__device__ __forceinline__ void store_out_h3(float* dst, f32x3 v) {
+  if constexpr (MANO_H3_NT_STORE) __builtin_nontemporal_store(v, reinterpret_cast<f32x3*>(dst));
+  else *reinterpret_cast<f32x3*>(dst) = v;
+}
+
 __device__ __forceinline__ void unit_range_h3(int64_t units, int64_t worker, int64_t n_workers,
                                               int64_t& begin, int64_t& end) {
   begin = worker * units / n_workers;
@@ -369,10 +377,8 @@ __global__ __launch_bounds__(64 * kH3Waves, kH3BlocksPerCU) void blend_skin_h3_k
         lbs_h3(F[t], w1, w2, p[t], t_unscale, tr[t], out);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          *reinterpret_cast<f32x3*>(vtile[t] + (roff[t][r] + voff)) = f32x3{out[0][r], out[1][r], out[2][r]};
-          if constexpr (kVposed)
-            *reinterpret_cast<f32x3*>(ptile[t] + (roff[t][r] + voff)) =
-                f32x3{p[t][0][r], p[t][1][r], p[t][2][r]};
+          store_out_h3(vtile[t] + (roff[t][r] + voff), f32x3{out[0][r], out[1][r], out[2][r]});
+          if constexpr (kVposed) store_out_h3(ptile[t] + (roff[t][r] + voff), f32x3{p[t][0][r], p[t][1][r], p[t][2][r]});
         }
       }
       // Group grp + 1 has landed in LDS (every wave's pieces) and every wave

@@ -97,6 +97,9 @@ __device__ __forceinline__ void put_rows(float* stage, int lane, const f32x4u (&
 
 // Stage -> HBM.  A row past the batch end holds the last hand's results and
 // re-writes them (identical bits) to that hand's row.
+#ifndef MANO_SPAN_ABLATE
+#define MANO_SPAN_ABLATE 0  // diagnostic: 1 = tile operands / weights fetched once, 2 = no LBS, 4 = NT stores
+#endif
 __device__ __forceinline__ void store_rows(const float* stage, float* __restrict__ tile, int vstride,
                                            int v0, int n_valid, int lane) {
 #pragma unroll
@@ -105,7 +108,8 @@ __device__ __forceinline__ void store_rows(const float* stage, float* __restrict
     sweep_slot(i, lane, row, c4);
     const f32x4 v = *reinterpret_cast<const f32x4*>(stage + row * kStride + 4 * c4);
     const unsigned off = unsigned(min(row, n_valid - 1) * vstride + 4 * c4);
-    *reinterpret_cast<f32x4u*>(tile + 3 * v0 + off) = v;
+    if constexpr (MANO_SPAN_ABLATE & 4) __builtin_nontemporal_store(v, reinterpret_cast<f32x4u*>(tile + 3 * v0 + off));
+    else *reinterpret_cast<f32x4u*>(tile + 3 * v0 + off) = v;
   }
 }
 
@@ -220,6 +224,12 @@ __device__ __forceinline__ void run_units(Lbs& lbs, const float* __restrict__ vp
     return (uu + 1) % kChunk ? uu + 1 : uu + 1 + (n_workers - 1) * kChunk;
   };
   int64_t cur_tile = -1;
+  typename Lbs::W w_once[kGroups];
+  if constexpr ((MANO_SPAN_ABLATE & 1) && Lbs::kInPlace) {
+    lbs.fetch_tile(0, n, 16, lane, lbs.cur);
+#pragma unroll
+    for (int g = 0; g < kGroups; ++g) w_once[g] = lbs.load_w(g, lane);
+  }
   fetch_rows(u_begin);
   for (int64_t uu = u_begin; uu < u_end; uu = next_unit(uu)) {
     const int64_t tile = uu / spans;
@@ -232,14 +242,15 @@ __device__ __forceinline__ void run_units(Lbs& lbs, const float* __restrict__ vp
     // Lbs::kInPlace: the operands load straight into the current ones (the
     // previous unit's are dead here), so no second copy is live.
     typename Lbs::Tile tops;
-    if (new_tile) {
+    if (new_tile && !((MANO_SPAN_ABLATE & 1) && Lbs::kInPlace)) {
       if constexpr (Lbs::kInPlace) lbs.fetch_tile(h0, n, n_valid, lane, lbs.cur);
       else lbs.fetch_tile(h0, n, n_valid, lane, tops);
     }
     typename Lbs::W w[kGroups];
 #pragma unroll
     for (int g = 0; g < kGroups; ++g)
-      if (full || g < n_tail) w[g] = lbs.load_w(kGroups * (full ? s : n_full) + g, lane);
+      if constexpr ((MANO_SPAN_ABLATE & 1) && Lbs::kInPlace) w[g] = w_once[g];
+      else if (full || g < n_tail) w[g] = lbs.load_w(kGroups * (full ? s : n_full) + g, lane);
     if (full) {
       put_rows(stage, lane, buf);
       if (!Lbs::kInPlace && new_tile) lbs.set_tile(tops);
@@ -251,7 +262,14 @@ __device__ __forceinline__ void run_units(Lbs& lbs, const float* __restrict__ vp
       for (int g = 0; g < kGroups; ++g) {
         float p[4][3], o[4][3];
         read_points(stage, lane, g, p);
-        lbs.apply(w[g], p, o);
+        if constexpr ((MANO_SPAN_ABLATE & 2) && Lbs::kInPlace) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) o[r][c] = p[r][c] + w[g][r];
+        } else {
+          lbs.apply(w[g], p, o);
+        }
         write_points(stage, lane, g, o);
         __builtin_amdgcn_sched_barrier(0);  // one group's LBS temporaries live at a time
       }

@@ -35,6 +35,13 @@ for prec in ("fp32", "f16x3"):
     ms_art = float(np.mean([a.elapsed_time(b) for a, b in ev2]))
     if ref is None:
         ref = v.clone()
+        # the default library's fp32 result, for the other builds' "vs default"
+        refp = "/tmp/time_forward_ref.pt"
+        if os.path.basename(_abi.LIB_PATH) == "libmano_hip.so":
+            torch.save(ref[:, :778].cpu(), refp)
+        if os.path.exists(refp):
+            d = (ref[:, :778].cpu() - torch.load(refp, weights_only=True)).abs().max().item()
+            print(f"{os.path.basename(_abi.LIB_PATH):24s} fp32 vs default build max {d:.2e}", flush=True)
     err = (v[:, :778] - ref[:, :778]).abs().max().item()
     print(f"{os.path.basename(_abi.LIB_PATH):24s} {prec:6s} blend_skin {ms:.4f} ms  articulate {ms_art:.4f} ms  "
           f"vs fp32 max {err:.2e}", flush=True)
