@@ -79,6 +79,12 @@ hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* featu
 hipError_t launch_skin(const DeviceModel& m, int64_t n, const float* transforms,
                        const float* vposed, const float* trans, float* verts,
                        hipStream_t stream);
+// The 4-hand-unit fp32 LBS (mano_skin_quad.hip); launch_skin uses it when
+// skin_quad_supported(m) (16 <= V <= 1024).
+bool skin_quad_supported(const DeviceModel& m);
+hipError_t launch_skin_quad(const DeviceModel& m, int64_t n, const float* transforms,
+                            const float* vposed, const float* trans, float* verts,
+                            hipStream_t stream);
 // f16x3 mode (mano_kernels_h3.hip): same operands and outputs as
 // launch_blend_skin / launch_skin.
 hipError_t launch_blend_skin_h3(const DeviceModel& m, int64_t n, const float* features,

@@ -1218,6 +1218,11 @@ hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* featu
   return hipGetLastError();
 }
 
+// fp32 standalone LBS: skin_quad (mano_skin_quad.hip) by default; skin_span
+// (above) for meshes it does not take, or with MANO_SKIN_QUAD=0.
+#ifndef MANO_SKIN_QUAD
+#define MANO_SKIN_QUAD 1
+#endif
 hipError_t launch_skin(const DeviceModel& m, int64_t n, const float* transforms,
                        const float* vposed, const float* trans, float* verts,
                        hipStream_t stream) {
@@ -1245,6 +1250,9 @@ hipError_t launch_skin(const DeviceModel& m, int64_t n, const float* transforms,
     else launch(skin_ring_kernel<false>);
     return hipGetLastError();
   }
+#endif
+#if MANO_SKIN_QUAD
+  if (skin_quad_supported(m)) return launch_skin_quad(m, n, transforms, vposed, trans, verts, stream);
 #endif
   const int64_t units = (n + 15) / 16 * span::n_spans(m.n_verts);
   auto launch = [&](auto kernel) {

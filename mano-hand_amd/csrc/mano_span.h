@@ -113,6 +113,18 @@ __device__ __forceinline__ void store_rows(const float* stage, float* __restrict
   }
 }
 
+// Diagnostic (MANO_SPAN_ABLATE & 8): registers -> HBM in the same sweep.
+__device__ __forceinline__ void store_regs(const f32x4u (&buf)[kF4], float* __restrict__ tile, int vstride,
+                                           int v0, int n_valid, int lane) {
+#pragma unroll
+  for (int i = 0; i < kF4; ++i) {
+    int row, c4;
+    sweep_slot(i, lane, row, c4);
+    const unsigned off = unsigned(min(row, n_valid - 1) * vstride + 4 * c4);
+    *reinterpret_cast<f32x4u*>(tile + 3 * v0 + off) = buf[i];
+  }
+}
+
 // The lane's points of group g in the MFMA D layout: p[r] = vertex 16 g + col
 // of hand row 4q + r.
 __device__ __forceinline__ void read_points(const float* stage, int lane, int g, float (&p)[4][3]) {
@@ -251,6 +263,16 @@ __device__ __forceinline__ void run_units(Lbs& lbs, const float* __restrict__ vp
     for (int g = 0; g < kGroups; ++g)
       if constexpr ((MANO_SPAN_ABLATE & 1) && Lbs::kInPlace) w[g] = w_once[g];
       else if (full || g < n_tail) w[g] = lbs.load_w(kGroups * (full ? s : n_full) + g, lane);
+    if constexpr ((MANO_SPAN_ABLATE & 8) && Lbs::kInPlace) {
+      if (full) {  // plain copy of the unit's rows, no LDS, no LBS
+        f32x4u cp[kF4];
+#pragma unroll
+        for (int i = 0; i < kF4; ++i) cp[i] = buf[i];
+        if (next_unit(uu) < u_end) fetch_rows(next_unit(uu));
+        store_regs(cp, verts + h0 * vstride, vstride, kVerts * s, n_valid, lane);
+        continue;
+      }
+    }
     if (full) {
       put_rows(stage, lane, buf);
       if (!Lbs::kInPlace && new_tile) lbs.set_tile(tops);
