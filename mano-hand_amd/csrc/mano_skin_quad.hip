@@ -336,6 +336,197 @@ __global__ __launch_bounds__(64 * kQWaves, 1) void skin_quad_kernel(
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// skin_quad_direct (MANO_QUAD_DIRECT): the same units and transposed blend,
+// but each lane loads exactly what it uses straight into registers -- per
+// group and tile the 12-B point of its (hand, vertex) (a wave's load covers
+// the 192-B row segments of 1-2 hands; the lanes of one vertex's three
+// coordinates read the same 12 B), its 12 A-operand words and its
+// translation word -- and stores its one output word per group and tile.  No
+// LDS staging: the next unit's loads are issued before this unit's MFMAs
+// (ping-pong register sets), every unit issues the same loads and stores
+// (tail groups and hands past the batch end are clamped duplicates that
+// rewrite identical bits), so hipcc's wait before a unit's MFMAs leaves the
+// previous unit's stores and the next unit's loads in flight.
+// ---------------------------------------------------------------------------
+#ifndef MANO_QUAD_DIRECT
+#define MANO_QUAD_DIRECT 0
+#endif
+#ifndef MANO_QUAD_DIRECT_WAVES
+#define MANO_QUAD_DIRECT_WAVES 4  // one wave per SIMD
+#endif
+constexpr int kQdWaves = MANO_QUAD_DIRECT_WAVES;
+
+struct QuadRegs {
+  f32x3 p[4][3];  // point of (hand hh[t], vertex vb_g + v)
+  float a[3][4];  // A operand of step k: transforms of row 16 t + v, joint 4 k + q
+  float tr[3];    // translation of (hand hh[t], coordinate cc[t])
+};
+
+template <bool kTrans>
+__global__ __launch_bounds__(64 * kQdWaves, 1) void skin_quad_direct_kernel(
+    const float* __restrict__ transforms, const float* __restrict__ wfrag16,
+    const float* __restrict__ vposed, const float* __restrict__ trans, float* __restrict__ verts,
+    int64_t n, int n_verts, int n_groups) {
+  __shared__ f32x4 w_lds[kQMaxGroups * 64];
+  for (int i = threadIdx.x; i < n_groups * 64; i += 64 * kQdWaves)
+    w_lds[i] = reinterpret_cast<const f32x4*>(wfrag16)[i];
+  __syncthreads();
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+v"(lane));
+  const int vstride = 3 * n_verts;
+  const int n_full = n_verts / kQVerts;
+  const int n_tail = n_groups - 4 * n_full;
+  const int spans = n_full + (n_tail > 0 ? 1 : 0);
+  const int64_t n_quads = (n + kQHands - 1) / kQHands;
+  const int64_t b = blockIdx.x, nb = gridDim.x;
+  const int64_t blk = (nb % 8) ? b : (b % 8) * (nb / 8) + b / 8;
+  const int64_t worker = blk * kQdWaves + wave, n_workers = nb * kQdWaves;
+  const int64_t step_q = n_workers / spans;
+  const int step_s = int(n_workers - step_q * spans);
+
+  const int q = lane >> 4, v = lane & 15;
+  int hh[3], cc[3], ah[3], aoff[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int m0 = 16 * t + 4 * q, m = 16 * t + v;
+    hh[t] = m0 / 12;
+    cc[t] = (m0 % 12) / 4;
+    ah[t] = m / 12;
+    aoff[t] = 12 * q + m % 12;
+  }
+  auto group_of = [&](int s, int g) { return s < n_full ? 4 * s + g : 4 * n_full + min(g, n_tail - 1); };
+  auto vbase_of = [&](int G) { return min(16 * G, n_verts - 16); };
+
+  // Buffer resources per unit (SGPR base = the quad's first row), per-lane
+  // 32-bit voffsets, per-group soffsets: the addressing costs a few scalar
+  // ops and one VALU op per tile, not 64-bit VALU address math per load.
+  constexpr int kRsrcFlags = 0x00020000;  // gfx9 raw buffer, 32-bit dwords
+  auto rsrc = [&](const float* base, int64_t floats) {
+    const int64_t bytes = floats * 4;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0,
+                                             int(bytes < 0x7fffffff ? bytes : 0x7fffffff), kRsrcFlags);
+  };
+  auto fetch = [&](int64_t qd, int s, QuadRegs& r) {
+    const int64_t h0 = qd * kQHands;
+    const int last = int(n - h0 < kQHands ? n - h0 : kQHands) - 1;
+    const auto rv = rsrc(vposed + h0 * vstride, int64_t(last + 1) * vstride);
+    const auto rt = rsrc(transforms + h0 * kTransformFloats, int64_t(last + 1) * kTransformFloats);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const int voff = 4 * (min(hh[t], last) * vstride + 3 * v);
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        r.p[g][t] = __builtin_bit_cast(f32x3, __builtin_amdgcn_raw_buffer_load_b96(
+                                                  rv, voff, 12 * vbase_of(group_of(s, g)), 0));
+      const int aofs = 4 * (min(ah[t], last) * kTransformFloats + aoff[t]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        r.a[t][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rt, aofs, 4 * 48 * k, 0));
+      if constexpr (kTrans) {
+        const auto rr = rsrc(trans + h0 * 3, int64_t(last + 1) * 3);
+        r.tr[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, 4 * (min(hh[t], last) * 3 + cc[t]), 0, 0));
+      }
+    }
+  };
+
+  // The stored words and their voffsets stay live until after the next
+  // fetch (keep_live), so the next unit's loads never land in a register a
+  // store still reads (hipcc would wait for that store first).
+  float out[12];
+  int out_off[3];
+  auto keep_live = [&] {
+#pragma unroll
+    for (int i = 0; i < 12; ++i) asm volatile("" ::"v"(out[i]));
+#pragma unroll
+    for (int i = 0; i < 3; ++i) asm volatile("" ::"v"(out_off[i]));
+  };
+  auto compute = [&](int64_t qd, int s, const QuadRegs& r) {
+    const int64_t h0 = qd * kQHands;
+    const int last = int(n - h0 < kQHands ? n - h0 : kQHands) - 1;
+    const auto ro = rsrc(verts + h0 * vstride, int64_t(last + 1) * vstride);
+    f32x4 wf[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) wf[g] = w_lds[group_of(s, g) * 64 + lane];
+    f32x4 T[4][3];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+          T[g][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(r.a[t][k], wf[g][k], k == 0 ? f32x4{} : T[g][t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      out_off[t] = 4 * (min(hh[t], last) * vstride + 3 * v + cc[t]);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float o = T[g][t][3];
+        o = fmaf(T[g][t][2], r.p[g][t][2], o);
+        o = fmaf(T[g][t][1], r.p[g][t][1], o);
+        o = fmaf(T[g][t][0], r.p[g][t][0], o);
+        if constexpr (kTrans) o = o + r.tr[t];
+        out[4 * t + g] = o;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), ro, out_off[t],
+                                              12 * vbase_of(group_of(s, g)), 0);
+      }
+    }
+  };
+
+  auto advance = [&](int64_t& aq, int& as) {
+    aq += step_q;
+    as += step_s;
+    if (as >= spans) {
+      as -= spans;
+      ++aq;
+    }
+  };
+  // Program order of the memory operations, kept by the IR passes (memory
+  // clobber) and the machine scheduler (sched_barrier).
+  auto order_point = [] {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  int64_t qd = worker / spans;
+  int s = int(worker - qd * spans);
+  if (qd >= n_quads) return;
+  // Ping-pong register sets; the next unit's fetch is unconditional (past the
+  // end it re-fetches the current unit), so every step issues the same loads.
+  QuadRegs ra, rb;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) out[i] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) out_off[i] = 0;
+  fetch(qd, s, ra);
+  for (;;) {
+    int64_t q1 = qd;
+    int s1 = s;
+    advance(q1, s1);
+    const bool more1 = q1 < n_quads;
+    fetch(more1 ? q1 : qd, more1 ? s1 : s, rb);
+    keep_live();
+    order_point();  // the next unit's loads go out before this unit's MFMAs
+    compute(qd, s, ra);
+    order_point();
+    if (!more1) break;
+    qd = q1;
+    s = s1;
+    advance(q1, s1);
+    const bool more2 = q1 < n_quads;
+    fetch(more2 ? q1 : qd, more2 ? s1 : s, ra);
+    keep_live();
+    order_point();
+    compute(qd, s, rb);
+    order_point();
+    if (!more2) break;
+    qd = q1;
+    s = s1;
+  }
+}
+
 }  // namespace
 
 bool skin_quad_supported(const DeviceModel& m) {
@@ -353,6 +544,16 @@ hipError_t launch_skin_quad(const DeviceModel& m, int64_t n, const float* transf
   int64_t blocks = (units + kQWaves - 1) / kQWaves;
   const int64_t cap = m.n_cu > 0 ? m.n_cu : 1;
   if (blocks > cap) blocks = cap;
+#if MANO_QUAD_DIRECT
+  blocks = std::min<int64_t>((units + kQdWaves - 1) / kQdWaves, cap);
+  auto launch = [&](auto kernel) {
+    hipLaunchKernelGGL(kernel, dim3(unsigned(blocks)), dim3(64 * kQdWaves), 0, stream, transforms,
+                       m.wfrag16, vposed, trans, verts, n, m.n_verts, m.n_groups16);
+  };
+  if (trans) launch(skin_quad_direct_kernel<true>);
+  else launch(skin_quad_direct_kernel<false>);
+  return hipGetLastError();
+#else
   auto launch = [&](auto kernel) {
     hipLaunchKernelGGL(kernel, dim3(unsigned(blocks)), dim3(64 * kQWaves), 0, stream, transforms,
                        m.wfrag16, vposed, trans, verts, n, m.n_verts, m.n_groups16);
@@ -360,6 +561,7 @@ hipError_t launch_skin_quad(const DeviceModel& m, int64_t n, const float* transf
   if (trans) launch(skin_quad_kernel<true>);
   else launch(skin_quad_kernel<false>);
   return hipGetLastError();
+#endif
 }
 
 }  // namespace mano
