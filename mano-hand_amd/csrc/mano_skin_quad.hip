@@ -21,17 +21,26 @@
 // B fragments (wfrag16), the same fmaf chains -- the results are bit-identical
 // to the fused kernel's (tests/test_gpu_parity.py fused == unfused).
 //
-// Per block (one per CU, kQWaves waves): every group's W fragment resident in
-// LDS (n_groups16 KB, loaded once), and per wave a stage of the unit's rows
-// (row stride 196 floats) and its 4 hands' transforms.  The next unit's rows,
-// transforms and translations are loaded into registers before the current
-// unit is skinned.  Vertices past the last full span (n_verts % 64) form the
-// tail unit of each hand quad: its 16-vertex groups (the last one shifted to
-// end at n_verts, as the packed W fragments are) load and store their points
-// straight from HBM.
+// Two kernels share these units and this arithmetic:
+//   skin_pair_kernel (default): per SIMD one memory wave (v_posed rows and
+//     the 4 hands' transforms -> an LDS stage slot; skinned slot -> verts)
+//     and two compute waves (slot -> MFMA -> slot, alternate units), four
+//     slots per memory wave handed over through LDS counters -- the HBM
+//     stream runs at one streaming wave per SIMD, the span_rows optimum,
+//     with the MFMA work beside it.  0.274-0.276 ms at 65,536 hands (trans),
+//     58 % of 8 TB/s (tools/debug/time_skin.py).
+//   skin_quad_kernel (MANO_QUAD_PAIR=0): every wave does both roles for its
+//     own units, 2 waves per SIMD: 0.286-0.291 ms.
+// Per block (one per CU): every group's W fragment resident in LDS (n_groups16
+// KB, loaded once) and per unit a stage of its rows (row stride 196 floats)
+// and its 4 hands' transforms.  Vertices past the last full span
+// (n_verts % 64) form the tail unit of each hand quad: its segment starts at
+// min(64 n_full, n_verts - 16) and its 16-vertex groups sit where the packed
+// W fragments put them (the mesh's last group shifted to end at n_verts).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
 
 #include "mano_internal.h"
 
@@ -82,19 +91,41 @@ __device__ __forceinline__ void wave_sync() {
   asm volatile("" ::: "memory");
 }
 
-// One (hand, coordinate) output of lane (q, v): the 4 MFMAs of its tile's
-// transform blend over K = 16 joints, then the apply in blend_skin16's order.
-__device__ __forceinline__ float lbs_quad(const float (&a)[4], const f32x4& wf, float x, float y,
-                                          float z) {
-  f32x4 T = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], wf[0], f32x4{}, 0, 0, 0);
-  T = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], wf[1], T, 0, 0, 0);
-  T = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], wf[2], T, 0, 0, 0);
-  T = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], wf[3], T, 0, 0, 0);
-  float o = T[3];
-  o = fmaf(T[2], z, o);
-  o = fmaf(T[1], y, o);
-  o = fmaf(T[0], x, o);
-  return o;
+// NG groups (G[0..NG)): the full units and a 1-group tail skip the
+// duplicates a multi-group tail needs.
+template <bool kTrans, int NG = 4>
+__device__ __forceinline__ void skin_unit4(QuadStage& st, const f32x4* w_lds, const float (&a)[3][4],
+                                           const float (&tr3)[3], const int (&G)[4], const int (&lv)[4],
+                                           const int (&hh)[3], const int (&cc)[3], int v, int lane) {
+  f32x4 wf[NG];
+  float p[NG][3][3];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) wf[g] = w_lds[G[g] * 64 + lane];
+#pragma unroll
+  for (int g = 0; g < NG; ++g)
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) p[g][t][c] = st.rows[hh[t] * kQStride + 3 * (lv[g] + v) + c];
+  f32x4 T[NG][3];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+        T[g][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][k], wf[g][k], k == 0 ? f32x4{} : T[g][t], 0, 0, 0);
+#pragma unroll
+  for (int g = 0; g < NG; ++g)
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      float o = T[g][t][3];
+      o = fmaf(T[g][t][2], p[g][t][2], o);
+      o = fmaf(T[g][t][1], p[g][t][1], o);
+      o = fmaf(T[g][t][0], p[g][t][0], o);
+      if constexpr (kTrans) o = o + tr3[t];
+      st.rows[hh[t] * kQStride + 3 * (lv[g] + v) + cc[t]] = o;
+    }
 }
 
 template <bool kTrans>
@@ -217,25 +248,6 @@ __global__ __launch_bounds__(64 * kQWaves, 1) void skin_quad_kernel(
 #pragma unroll
     for (int i = 0; i < kQF4; ++i) *reinterpret_cast<f32x4*>(st.rows + so[i]) = rb[i];
   };
-  // One group's LBS: points from the stage, outputs back in place (every
-  // lane's points are read -- in-order LDS -- before any output lands).
-  auto skin_group = [&](const float (&a)[3][4], const float (&tr3)[3], int wgrp, int lv) {
-    const f32x4 wf = w_lds[wgrp * 64 + lane];
-    float p[3][3], o[3];
-#pragma unroll
-    for (int t = 0; t < 3; ++t)
-#pragma unroll
-      for (int c = 0; c < 3; ++c) p[t][c] = st.rows[hh[t] * kQStride + 3 * (lv + v) + c];
-#pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      o[t] = lbs_quad(a[t], wf, p[t][0], p[t][1], p[t][2]);
-      if constexpr (kTrans) o[t] = o[t] + tr3[t];
-    }
-#pragma unroll
-    for (int t = 0; t < 3; ++t) st.rows[hh[t] * kQStride + 3 * (lv + v) + cc[t]] = o[t];
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
   // Unit (qd, s): its operands and rows go registers -> LDS stage, the next
   // unit is fetched, the unit is skinned and stored.  The next unit's stage
   // hand-off sits after this unit's stores, so its wait (vmcnt(3): all but
@@ -263,47 +275,21 @@ __global__ __launch_bounds__(64 * kQWaves, 1) void skin_quad_kernel(
       for (int k = 0; k < 4; ++k) a[t][k] = st.tr[a_off[t] + 4 * 12 * k];
       tr3[t] = kTrans ? st.trans[3 * hh[t] + cc[t]] : 0.f;
     }
-    if (MANO_QUAD_ABLATE & 1) {
-      // diagnostic: no LBS (the stage streams out unchanged)
-    } else if (full) {
-      // The unit's 4 groups at once: 12 independent 4-MFMA chains issued
-      // step-major (no chain waits on its own previous MFMA), every point
-      // and W fragment read up front -- one wave per SIMD has the registers,
-      // and its compute per unit must stay under the row stream's latency.
-      f32x4 wf[4];
-      float p[4][3][3];
+    if (!(MANO_QUAD_ABLATE & 1)) {  // diagnostic 1: no LBS (the stage streams out unchanged)
+      if (full) {
+        const int G[4] = {4 * s, 4 * s + 1, 4 * s + 2, 4 * s + 3};
+        const int lv[4] = {0, 16, 32, 48};
+        skin_unit4<kTrans>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
+      } else {
+        int G[4], lv[4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) wf[g] = w_lds[(4 * s + g) * 64 + lane];
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-#pragma unroll
-        for (int t = 0; t < 3; ++t)
-#pragma unroll
-          for (int c = 0; c < 3; ++c) p[g][t][c] = st.rows[hh[t] * kQStride + 48 * g + 3 * v + c];
-      f32x4 T[4][3];
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-#pragma unroll
-          for (int t = 0; t < 3; ++t)
-            T[g][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][k], wf[g][k], k == 0 ? f32x4{} : T[g][t], 0, 0, 0);
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-#pragma unroll
-        for (int t = 0; t < 3; ++t) {
-          float o = T[g][t][3];
-          o = fmaf(T[g][t][2], p[g][t][2], o);
-          o = fmaf(T[g][t][1], p[g][t][1], o);
-          o = fmaf(T[g][t][0], p[g][t][0], o);
-          if constexpr (kTrans) o = o + tr3[t];
-          st.rows[hh[t] * kQStride + 48 * g + 3 * v + cc[t]] = o;
+        for (int g = 0; g < 4; ++g) {
+          G[g] = 4 * n_full + min(g, n_tail - 1);
+          lv[g] = min(16 * G[g], n_verts - 16) - tail_v0;
         }
-    } else {
-      // the tail's groups, at the packed W fragments' placement (the mesh's
-      // last group shifted to end at n_verts)
-      for (int g = 0; g < n_tail; ++g)
-        skin_group(a, tr3, 4 * n_full + g, min(16 * (4 * n_full + g), n_verts - 16) - tail_v0);
+        if (n_tail == 1) skin_unit4<kTrans, 1>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
+        else skin_unit4<kTrans>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
+      }
     }
     wave_sync();
     float* dst = verts + h0 * vstride + 3 * v0;
@@ -338,43 +324,79 @@ __global__ __launch_bounds__(64 * kQWaves, 1) void skin_quad_kernel(
 
 
 // ---------------------------------------------------------------------------
-// skin_quad_direct (MANO_QUAD_DIRECT): the same units and transposed blend,
-// but each lane loads exactly what it uses straight into registers -- per
-// group and tile the 12-B point of its (hand, vertex) (a wave's load covers
-// the 192-B row segments of 1-2 hands; the lanes of one vertex's three
-// coordinates read the same 12 B), its 12 A-operand words and its
-// translation word -- and stores its one output word per group and tile.  No
-// LDS staging: the next unit's loads are issued before this unit's MFMAs
-// (ping-pong register sets), every unit issues the same loads and stores
-// (tail groups and hands past the batch end are clamped duplicates that
-// rewrite identical bits), so hipcc's wait before a unit's MFMAs leaves the
-// previous unit's stores and the next unit's loads in flight.
+// skin_pair_kernel: skin_quad's units with the roles split per SIMD.  Memory
+// wave w (0..3) stages unit k into slot k % kPairSlots, signals full = k + 1,
+// loads unit k + 1, then stores unit k - kPairCompute once its slot's done
+// counter says it is skinned; compute wave c of pair w (wave 4 + 4c + w,
+// same SIMD) skins units c, c + kPairCompute, ... in place and sets the
+// slot's done counter.  Measured (65,536 hands): one compute wave per
+// memory wave 0.335-0.374 ms (the compute side is the bottleneck), two
+// 0.274-0.276, the memory waves alone (no LBS) 0.241-0.265.
 // ---------------------------------------------------------------------------
-#ifndef MANO_QUAD_DIRECT
-#define MANO_QUAD_DIRECT 0
+#ifndef MANO_QUAD_PAIR
+#define MANO_QUAD_PAIR 1  // the default standalone LBS; 0 = skin_quad_kernel
 #endif
-#ifndef MANO_QUAD_DIRECT_WAVES
-#define MANO_QUAD_DIRECT_WAVES 4  // one wave per SIMD
+#ifndef MANO_QUAD_PAIR_COMPUTE
+#define MANO_QUAD_PAIR_COMPUTE 2  // compute waves per memory wave (same SIMD)
 #endif
-constexpr int kQdWaves = MANO_QUAD_DIRECT_WAVES;
+// memory waves 0..3, compute waves 4..; wave w runs on SIMD w % 4
+#ifndef MANO_QUAD_PAIR_PRIO
+#define MANO_QUAD_PAIR_PRIO 0  // issue priority of the memory waves
+#endif
+constexpr int kPairs = 4;
+constexpr int kPairCompute = MANO_QUAD_PAIR_COMPUTE;
+constexpr int kPairSlots = 2 * kPairCompute;
+constexpr int kPairWaves = kPairs * (1 + kPairCompute);
+constexpr int kPairMaxGroups = 52;  // W in LDS beside the slots: V <= 832
 
-struct QuadRegs {
-  f32x3 p[4][3];  // point of (hand hh[t], vertex vb_g + v)
-  float a[3][4];  // A operand of step k: transforms of row 16 t + v, joint 4 k + q
-  float tr[3];    // translation of (hand hh[t], coordinate cc[t])
+struct PairShared {
+  QuadStage slot[kPairs][kPairSlots];
+  int full[kPairs];               // units staged
+  int done[kPairs][kPairSlots];   // per slot: 1 + the last unit skinned in it
 };
 
+// The hand-over counters are read and written with inline ds_read/ds_write:
+// a volatile C++ access would make hipcc wait for every outstanding memory
+// operation (vmcnt(0)) -- the memory wave's loads and stores in flight.
+__device__ __forceinline__ unsigned lds_addr(const int* p) {
+  typedef const __attribute__((address_space(3))) int* lds_ptr;
+  return unsigned(reinterpret_cast<uintptr_t>((lds_ptr)p));  // generic -> LDS address (32 bit)
+}
+// Bounded: false after ~2^20 polls (tens of ms), and the caller then stops
+// -- a lost hand-over ends the kernel with wrong results, never hangs it.
+__device__ __forceinline__ bool pair_wait_ge(const int* flag, int target) {
+  const unsigned a = lds_addr(flag);
+  for (int it = 0; it < (1 << 20); ++it) {
+    int x;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(x) : "v"(a) : "memory");
+    if (__builtin_amdgcn_readfirstlane(x) >= target) return true;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return false;
+}
+__device__ __forceinline__ void pair_signal(int* flag, int value) {
+  // the slot's LDS writes have landed before the counter moves
+  asm volatile("s_waitcnt lgkmcnt(0)\n\tds_write_b32 %0, %1" ::"v"(lds_addr(flag)), "v"(value) : "memory");
+}
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
 template <bool kTrans>
-__global__ __launch_bounds__(64 * kQdWaves, 1) void skin_quad_direct_kernel(
+__global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     const float* __restrict__ transforms, const float* __restrict__ wfrag16,
     const float* __restrict__ vposed, const float* __restrict__ trans, float* __restrict__ verts,
     int64_t n, int n_verts, int n_groups) {
-  __shared__ f32x4 w_lds[kQMaxGroups * 64];
-  for (int i = threadIdx.x; i < n_groups * 64; i += 64 * kQdWaves)
+  __shared__ f32x4 w_lds[kPairMaxGroups * 64];
+  __shared__ PairShared sh;
+  for (int i = threadIdx.x; i < n_groups * 64; i += 64 * kPairWaves)
     w_lds[i] = reinterpret_cast<const f32x4*>(wfrag16)[i];
+  if (threadIdx.x < kPairs) sh.full[threadIdx.x] = 0;
+  if (threadIdx.x < kPairs * kPairSlots) sh.done[threadIdx.x / kPairSlots][threadIdx.x % kPairSlots] = 0;
   __syncthreads();
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int pair = wave & (kPairs - 1);
+  const bool is_mem = wave < kPairs;
   int lane = threadIdx.x & 63;
   asm volatile("" : "+v"(lane));
   const int vstride = 3 * n_verts;
@@ -384,98 +406,9 @@ __global__ __launch_bounds__(64 * kQdWaves, 1) void skin_quad_direct_kernel(
   const int64_t n_quads = (n + kQHands - 1) / kQHands;
   const int64_t b = blockIdx.x, nb = gridDim.x;
   const int64_t blk = (nb % 8) ? b : (b % 8) * (nb / 8) + b / 8;
-  const int64_t worker = blk * kQdWaves + wave, n_workers = nb * kQdWaves;
+  const int64_t worker = blk * kPairs + pair, n_workers = nb * kPairs;
   const int64_t step_q = n_workers / spans;
   const int step_s = int(n_workers - step_q * spans);
-
-  const int q = lane >> 4, v = lane & 15;
-  int hh[3], cc[3], ah[3], aoff[3];
-#pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    const int m0 = 16 * t + 4 * q, m = 16 * t + v;
-    hh[t] = m0 / 12;
-    cc[t] = (m0 % 12) / 4;
-    ah[t] = m / 12;
-    aoff[t] = 12 * q + m % 12;
-  }
-  auto group_of = [&](int s, int g) { return s < n_full ? 4 * s + g : 4 * n_full + min(g, n_tail - 1); };
-  auto vbase_of = [&](int G) { return min(16 * G, n_verts - 16); };
-
-  // Buffer resources per unit (SGPR base = the quad's first row), per-lane
-  // 32-bit voffsets, per-group soffsets: the addressing costs a few scalar
-  // ops and one VALU op per tile, not 64-bit VALU address math per load.
-  constexpr int kRsrcFlags = 0x00020000;  // gfx9 raw buffer, 32-bit dwords
-  auto rsrc = [&](const float* base, int64_t floats) {
-    const int64_t bytes = floats * 4;
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0,
-                                             int(bytes < 0x7fffffff ? bytes : 0x7fffffff), kRsrcFlags);
-  };
-  auto fetch = [&](int64_t qd, int s, QuadRegs& r) {
-    const int64_t h0 = qd * kQHands;
-    const int last = int(n - h0 < kQHands ? n - h0 : kQHands) - 1;
-    const auto rv = rsrc(vposed + h0 * vstride, int64_t(last + 1) * vstride);
-    const auto rt = rsrc(transforms + h0 * kTransformFloats, int64_t(last + 1) * kTransformFloats);
-#pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      const int voff = 4 * (min(hh[t], last) * vstride + 3 * v);
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        r.p[g][t] = __builtin_bit_cast(f32x3, __builtin_amdgcn_raw_buffer_load_b96(
-                                                  rv, voff, 12 * vbase_of(group_of(s, g)), 0));
-      const int aofs = 4 * (min(ah[t], last) * kTransformFloats + aoff[t]);
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        r.a[t][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rt, aofs, 4 * 48 * k, 0));
-      if constexpr (kTrans) {
-        const auto rr = rsrc(trans + h0 * 3, int64_t(last + 1) * 3);
-        r.tr[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, 4 * (min(hh[t], last) * 3 + cc[t]), 0, 0));
-      }
-    }
-  };
-
-  // The stored words and their voffsets stay live until after the next
-  // fetch (keep_live), so the next unit's loads never land in a register a
-  // store still reads (hipcc would wait for that store first).
-  float out[12];
-  int out_off[3];
-  auto keep_live = [&] {
-#pragma unroll
-    for (int i = 0; i < 12; ++i) asm volatile("" ::"v"(out[i]));
-#pragma unroll
-    for (int i = 0; i < 3; ++i) asm volatile("" ::"v"(out_off[i]));
-  };
-  auto compute = [&](int64_t qd, int s, const QuadRegs& r) {
-    const int64_t h0 = qd * kQHands;
-    const int last = int(n - h0 < kQHands ? n - h0 : kQHands) - 1;
-    const auto ro = rsrc(verts + h0 * vstride, int64_t(last + 1) * vstride);
-    f32x4 wf[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) wf[g] = w_lds[group_of(s, g) * 64 + lane];
-    f32x4 T[4][3];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-#pragma unroll
-        for (int t = 0; t < 3; ++t)
-          T[g][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(r.a[t][k], wf[g][k], k == 0 ? f32x4{} : T[g][t], 0, 0, 0);
-#pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      out_off[t] = 4 * (min(hh[t], last) * vstride + 3 * v + cc[t]);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float o = T[g][t][3];
-        o = fmaf(T[g][t][2], r.p[g][t][2], o);
-        o = fmaf(T[g][t][1], r.p[g][t][1], o);
-        o = fmaf(T[g][t][0], r.p[g][t][0], o);
-        if constexpr (kTrans) o = o + r.tr[t];
-        out[4 * t + g] = o;
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), ro, out_off[t],
-                                              12 * vbase_of(group_of(s, g)), 0);
-      }
-    }
-  };
-
   auto advance = [&](int64_t& aq, int& as) {
     aq += step_q;
     as += step_s;
@@ -484,52 +417,211 @@ __global__ __launch_bounds__(64 * kQdWaves, 1) void skin_quad_direct_kernel(
       ++aq;
     }
   };
-  // Program order of the memory operations, kept by the IR passes (memory
-  // clobber) and the machine scheduler (sched_barrier).
-  auto order_point = [] {
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  };
+  const int tail_v0 = min(kQVerts * n_full, n_verts - 16);
+  int* full_flag = &sh.full[pair];
   int64_t qd = worker / spans;
   int s = int(worker - qd * spans);
   if (qd >= n_quads) return;
-  // Ping-pong register sets; the next unit's fetch is unconditional (past the
-  // end it re-fetches the current unit), so every step issues the same loads.
-  QuadRegs ra, rb;
+
+  if (is_mem) {
+    if (MANO_QUAD_PAIR_PRIO) __builtin_amdgcn_s_setprio(MANO_QUAD_PAIR_PRIO);
+    // The memory wave shares its SIMD with the compute waves' f32 MFMAs,
+    // which hold the VALU datapath: every VALU op here waits for one.  So
+    // its per-unit work is buffer loads / stores and LDS accesses only --
+    // all lane offsets are kernel constants, the unit moves the SGPR buffer
+    // bases, and rows past the batch end fall outside num_records (loads
+    // read 0, stores are dropped) instead of being clamped.
+    const int tail_rf4 = 3 * (n_verts - tail_v0) / 4;
+    int fvo[kQF4], tvo[kQF4];                 // global byte offsets in the unit's rows
+    unsigned fso[kQF4], tso[kQF4], tro[kQTrF4];  // LDS byte addresses in slot 0
+    const unsigned slot0 = lds_addr(reinterpret_cast<const int*>(&sh.slot[pair][0]));
 #pragma unroll
-  for (int i = 0; i < 12; ++i) out[i] = 0.f;
+    for (int i = 0; i < kQF4; ++i) {
+      const int idx = 64 * i + lane;
+      const int fr = idx / kQRowF4, fc = 4 * (idx % kQRowF4);
+      const int it = min(idx, kQHands * tail_rf4 - 1);
+      const int tr = it / tail_rf4, tc = 4 * (it % tail_rf4);
+      fvo[i] = 4 * (fr * vstride + fc);
+      tvo[i] = 4 * (tr * vstride + tc);
+      fso[i] = slot0 + unsigned(offsetof(QuadStage, rows)) + 4u * unsigned(fr * kQStride + fc);
+      tso[i] = slot0 + unsigned(offsetof(QuadStage, rows)) + 4u * unsigned(tr * kQStride + tc);
+    }
 #pragma unroll
-  for (int i = 0; i < 3; ++i) out_off[i] = 0;
-  fetch(qd, s, ra);
-  for (;;) {
-    int64_t q1 = qd;
-    int s1 = s;
-    advance(q1, s1);
-    const bool more1 = q1 < n_quads;
-    fetch(more1 ? q1 : qd, more1 ? s1 : s, rb);
-    keep_live();
-    order_point();  // the next unit's loads go out before this unit's MFMAs
-    compute(qd, s, ra);
-    order_point();
-    if (!more1) break;
-    qd = q1;
-    s = s1;
-    advance(q1, s1);
-    const bool more2 = q1 < n_quads;
-    fetch(more2 ? q1 : qd, more2 ? s1 : s, ra);
-    keep_live();
-    order_point();
-    compute(qd, s, rb);
-    order_point();
-    if (!more2) break;
-    qd = q1;
-    s = s1;
+    for (int i = 0; i < kQTrF4; ++i) tro[i] = slot0 + unsigned(offsetof(QuadStage, tr)) + 16u * unsigned(64 * i + lane);
+    const unsigned trs = slot0 + unsigned(offsetof(QuadStage, trans)) + 4u * unsigned(min(lane, 15));
+    constexpr int kRsrcFlags = 0x00020000;  // gfx9 raw buffer
+    auto rsrc = [&](const float* base, int64_t floats) {
+      return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, int(floats * 4), kRsrcFlags);
+    };
+    f32x4 rb[kQF4], tb[kQTrF4];
+    float trb = 0.f;
+    auto fetch = [&](int64_t fq, int fs) {
+      const int64_t h0 = fq * kQHands;
+      const int valid = int(n - h0 < kQHands ? n - h0 : kQHands);
+      const auto rv = rsrc(vposed + h0 * vstride, int64_t(valid) * vstride);
+      const auto rt = rsrc(transforms + h0 * kTransformFloats, int64_t(valid) * kTransformFloats);
+#pragma unroll
+      for (int i = 0; i < kQTrF4; ++i)
+        tb[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * (64 * i + lane), 0, 0));
+      if constexpr (kTrans) {
+        const auto rr = rsrc(trans + h0 * 3, int64_t(valid) * 3);
+        trb = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, 4 * lane, 0, 0));
+      }
+      const bool full = fs < n_full;
+      const int soff = 4 * 3 * (full ? kQVerts * fs : tail_v0);
+#pragma unroll
+      for (int i = 0; i < kQF4; ++i)
+        rb[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, full ? fvo[i] : tvo[i], soff, 0));
+    };
+    auto ds_write4 = [](unsigned addr, const f32x4& v) {
+      *reinterpret_cast<__attribute__((address_space(3))) f32x4*>(uintptr_t(addr)) = v;
+    };
+    auto ds_read4 = [](unsigned addr) {
+      return *reinterpret_cast<const __attribute__((address_space(3))) f32x4*>(uintptr_t(addr));
+    };
+    constexpr unsigned kSlotBytes = sizeof(QuadStage);
+    auto stage = [&](int fs, unsigned slot) {
+      const unsigned so = slot * kSlotBytes;
+#pragma unroll
+      for (int i = 0; i < kQTrF4; ++i) ds_write4(tro[i] + so, tb[i]);
+      if constexpr (kTrans) {
+        if (lane < 12) *reinterpret_cast<__attribute__((address_space(3))) float*>(uintptr_t(trs + so)) = trb;
+      }
+      if (fs < n_full) {
+#pragma unroll
+        for (int i = 0; i < kQF4; ++i) ds_write4(fso[i] + so, rb[i]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < kQF4; ++i) ds_write4(tso[i] + so, rb[i]);
+      }
+    };
+    // The stored data stays live past the next unit's loads (keep_live), so
+    // those loads never reuse a register a store reads -- hipcc would first
+    // wait for that store.
+    f32x4 sdata[kQF4] = {};
+    auto keep_live = [&] {
+#pragma unroll
+      for (int i = 0; i < kQF4; ++i) asm volatile("" ::"v"(sdata[i]));
+    };
+    auto store = [&](int64_t fq, int fs, unsigned slot) {
+      const unsigned so = slot * kSlotBytes;
+      const int64_t h0 = fq * kQHands;
+      const int valid = int(n - h0 < kQHands ? n - h0 : kQHands);
+      const auto ro = rsrc(verts + h0 * vstride, int64_t(valid) * vstride);
+      const bool full = fs < n_full;
+      const int soff = 4 * 3 * (full ? kQVerts * fs : tail_v0);
+#pragma unroll
+      for (int i = 0; i < kQF4; ++i) sdata[i] = ds_read4((full ? fso[i] : tso[i]) + so);
+#pragma unroll
+      for (int i = 0; i < kQF4; ++i)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sdata[i]), ro, full ? fvo[i] : tvo[i], soff, 0);
+    };
+    // pend*: the units staged and not yet stored (0 = the latest)
+    int64_t pend_q[kPairCompute + 1];
+    int pend_s[kPairCompute + 1];
+    int k = 0;
+    bool ok = true;
+    auto stage_next = [&] {  // stage unit k, load unit k + 1
+      stage(s, unsigned(k % kPairSlots));
+      pair_signal(full_flag, k + 1);
+#pragma unroll
+      for (int i = kPairCompute; i > 0; --i) pend_q[i] = pend_q[i - 1], pend_s[i] = pend_s[i - 1];
+      pend_q[0] = qd;
+      pend_s[0] = s;
+      int64_t nq = qd;
+      int ns = s;
+      advance(nq, ns);
+      fetch(nq < n_quads ? nq : qd, nq < n_quads ? ns : s);
+      keep_live();
+      qd = nq;
+      s = ns;
+      ++k;
+    };
+    fetch(qd, s);
+    // The first kPairCompute units are staged without a store; then each
+    // iteration stores unit k - kPairCompute (once skinned) BEFORE staging
+    // unit k, so the stage's wait for unit k's loads leaves those stores in
+    // flight on every path into it (hipcc merges the wait counts of the
+    // paths: a path with no store after the loads would force vmcnt(0)).
+    for (int j = 0; j < kPairCompute && qd < n_quads; ++j) stage_next();
+    while (qd < n_quads) {
+      const int ku = k - kPairCompute;
+      if (!pair_wait_ge(&sh.done[pair][ku % kPairSlots], ku + 1)) {
+        ok = false;
+        break;
+      }
+      store(pend_q[kPairCompute - 1], pend_s[kPairCompute - 1], unsigned(ku % kPairSlots));
+      stage_next();
+    }
+    // the last min(k, kPairCompute) units
+    for (int i = min(k, kPairCompute) - 1; ok && i >= 0; --i) {
+      const int ku = k - 1 - i;
+      if (!pair_wait_ge(&sh.done[pair][ku % kPairSlots], ku + 1)) break;
+      store(pend_q[i], pend_s[i], unsigned(ku % kPairSlots));
+    }
+    return;
+  }
+
+  // compute wave
+  const int q = lane >> 4, v = lane & 15;
+  int hh[3], cc[3], a_off[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int m0 = 16 * t + 4 * q, m = 16 * t + v;
+    hh[t] = m0 / 12;
+    cc[t] = (m0 % 12) / 4;
+    a_off[t] = (m / 12) * kTransformFloats + 12 * q + m % 12;
+  }
+  // compute wave c of the pair takes the pair's units k = c, c + kPairCompute, ...
+  const int cw = (wave - kPairs) / kPairs;
+  for (int i = 0; i < cw; ++i) advance(qd, s);
+  for (int k = cw; qd < n_quads; k += kPairCompute) {
+    if (!pair_wait_ge(full_flag, k + 1)) return;
+    QuadStage& st = sh.slot[pair][k % kPairSlots];
+    if (MANO_QUAD_ABLATE & 2) {  // diagnostic: no compute (the memory waves alone)
+      pair_signal(&sh.done[pair][k % kPairSlots], k + 1);
+#pragma unroll
+      for (int i = 0; i < kPairCompute; ++i) advance(qd, s);
+      continue;
+    }
+    float a[3][4], tr3[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) a[t][kk] = st.tr[a_off[t] + 4 * 12 * kk];
+      tr3[t] = kTrans ? st.trans[3 * hh[t] + cc[t]] : 0.f;
+    }
+    // The unit's 4 groups (a tail unit: its n_tail groups, the last repeated
+    // -- duplicates rewrite identical bits).  Every point is read before any
+    // output lands: the tail's last group is shifted onto its neighbour's
+    // vertices when n_verts % 16 != 0, and the skinning is in place.  Full
+    // units get compile-time group offsets (LDS immediates).
+    if (s < n_full) {
+      const int G[4] = {4 * s, 4 * s + 1, 4 * s + 2, 4 * s + 3};
+      const int lv[4] = {0, 16, 32, 48};
+      skin_unit4<kTrans>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
+    } else {
+      int G[4], lv[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        G[g] = 4 * n_full + min(g, n_tail - 1);
+        lv[g] = min(16 * G[g], n_verts - 16) - tail_v0;
+      }
+      if (n_tail == 1) skin_unit4<kTrans, 1>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
+      else skin_unit4<kTrans>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
+    }
+    pair_signal(&sh.done[pair][k % kPairSlots], k + 1);
+#pragma unroll
+    for (int i = 0; i < kPairCompute; ++i) advance(qd, s);
   }
 }
 
 }  // namespace
 
 bool skin_quad_supported(const DeviceModel& m) {
+#if MANO_QUAD_PAIR
+  if (m.n_groups16 > kPairMaxGroups) return false;
+#endif
   // the tail segment must be whole float4 per row
   const int tail_v0 = std::min(kQVerts * (m.n_verts / kQVerts), m.n_verts - 16);
   return m.n_verts >= 16 && m.n_groups16 <= kQMaxGroups && (3 * (m.n_verts - tail_v0)) % 4 == 0;
@@ -544,14 +636,14 @@ hipError_t launch_skin_quad(const DeviceModel& m, int64_t n, const float* transf
   int64_t blocks = (units + kQWaves - 1) / kQWaves;
   const int64_t cap = m.n_cu > 0 ? m.n_cu : 1;
   if (blocks > cap) blocks = cap;
-#if MANO_QUAD_DIRECT
-  blocks = std::min<int64_t>((units + kQdWaves - 1) / kQdWaves, cap);
+#if MANO_QUAD_PAIR
+  blocks = std::min<int64_t>((units + kPairs - 1) / kPairs, cap);
   auto launch = [&](auto kernel) {
-    hipLaunchKernelGGL(kernel, dim3(unsigned(blocks)), dim3(64 * kQdWaves), 0, stream, transforms,
+    hipLaunchKernelGGL(kernel, dim3(unsigned(blocks)), dim3(64 * kPairWaves), 0, stream, transforms,
                        m.wfrag16, vposed, trans, verts, n, m.n_verts, m.n_groups16);
   };
-  if (trans) launch(skin_quad_direct_kernel<true>);
-  else launch(skin_quad_direct_kernel<false>);
+  if (trans) launch(skin_pair_kernel<true>);
+  else launch(skin_pair_kernel<false>);
   return hipGetLastError();
 #else
   auto launch = [&](auto kernel) {
