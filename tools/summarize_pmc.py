@@ -14,7 +14,7 @@ import sys
 from collections import defaultdict
 
 # demangled-name prefix -> bench.py kernel key
-KERNELS = {"blend_skin16_kernel<": "blend_skin", "blend_kernel(": "blend", "skin_span_kernel<": "skin",
+KERNELS = {"blend_skin16_kernel<": "blend_skin", "blend_kernel(": "blend", "skin_span_kernel<": "skin", "skin_pair_kernel<": "skin",
            "articulate_kernel<": "articulate", "blend_skin_h3_kernel<": "blend_skin_h3",
            "skin_span_h3_kernel<": "skin_h3"}
 # FETCH_SIZE correction (MI355X_MICROARCH.md §HBM): on gfx950 the counter
