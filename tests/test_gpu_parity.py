@@ -338,6 +338,26 @@ def test_fused_equals_unfused(engine, dev, params, B):
     assert np.abs(host(v) - ref["verts"]).max() <= TOL_M
 
 
+@pytest.mark.parametrize("B,with_trans", [(2, True), (3, False), (5, True), (1023, False),
+                                         (65537, True), (65538, False)])
+def test_standalone_lbs_ragged(engine, dev, params, B, with_trans):
+    """The standalone LBS (skin_pair: 4-hand units, a partial last quad when
+    B % 4 != 0, many units per memory wave at 65,537 hands) over a v_posed
+    buffer == the fused kernel's verts bit for bit; every vertex is written
+    and nothing past the batch (a NaN guard row after the output stays NaN)."""
+    rng = np.random.default_rng(300 + B)
+    betas = f32(rng.normal(0, 1, (B, 10)), dev)
+    pose = f32(rng.normal(0, 0.6, (B, 16, 3)), dev)
+    trans = f32(rng.uniform(-1, 1, (B, 3)), dev) if with_trans else None
+    fused = engine.forward(betas, pose, trans, rest_verts=True)
+    engine.stage_articulate(betas, pose, trans)
+    out = torch.full((B + 1, 778, 3), float("nan"), device=dev)
+    engine.stage_skin(B, out[:B], rest_verts=fused["rest_verts"], trans=trans)
+    torch.cuda.synchronize()
+    assert torch.equal(fused["verts"], out[:B])
+    assert torch.isnan(out[B]).all()
+
+
 @pytest.mark.parametrize("B,shared,with_trans", [(1, False, True), (17, True, False),
                                                  (200, False, False), (4096, False, True)])
 def test_forward_equals_staged(engine, dev, params, B, shared, with_trans):
