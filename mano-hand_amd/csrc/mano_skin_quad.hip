@@ -454,25 +454,30 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     auto rsrc = [&](const float* base, int64_t floats) {
       return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, int(floats * 4), kRsrcFlags);
     };
-    f32x4 rb[kQF4], tb[kQTrF4];
-    float trb = 0.f;
-    auto fetch = [&](int64_t fq, int fs) {
+    // Two register sets: the loads of unit k + 2 go out while unit k + 1's
+    // are in flight (set k & 1; the loop below is unrolled by 2 so the set is
+    // a compile-time choice -- a runtime-indexed pair would go to scratch).
+    struct MemRegs {
+      f32x4 rb[kQF4], tb[kQTrF4];
+      float trb;
+    };
+    auto fetch = [&](int64_t fq, int fs, MemRegs& R) {
       const int64_t h0 = fq * kQHands;
       const int valid = int(n - h0 < kQHands ? n - h0 : kQHands);
       const auto rv = rsrc(vposed + h0 * vstride, int64_t(valid) * vstride);
       const auto rt = rsrc(transforms + h0 * kTransformFloats, int64_t(valid) * kTransformFloats);
 #pragma unroll
       for (int i = 0; i < kQTrF4; ++i)
-        tb[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * (64 * i + lane), 0, 0));
+        R.tb[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * (64 * i + lane), 0, 0));
       if constexpr (kTrans) {
         const auto rr = rsrc(trans + h0 * 3, int64_t(valid) * 3);
-        trb = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, 4 * lane, 0, 0));
+        R.trb = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, 4 * lane, 0, 0));
       }
       const bool full = fs < n_full;
       const int soff = 4 * 3 * (full ? kQVerts * fs : tail_v0);
 #pragma unroll
       for (int i = 0; i < kQF4; ++i)
-        rb[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, full ? fvo[i] : tvo[i], soff, 0));
+        R.rb[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, full ? fvo[i] : tvo[i], soff, 0));
     };
     auto ds_write4 = [](unsigned addr, const f32x4& v) {
       *reinterpret_cast<__attribute__((address_space(3))) f32x4*>(uintptr_t(addr)) = v;
@@ -481,19 +486,19 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       return *reinterpret_cast<const __attribute__((address_space(3))) f32x4*>(uintptr_t(addr));
     };
     constexpr unsigned kSlotBytes = sizeof(QuadStage);
-    auto stage = [&](int fs, unsigned slot) {
+    auto stage = [&](int fs, unsigned slot, const MemRegs& R) {
       const unsigned so = slot * kSlotBytes;
 #pragma unroll
-      for (int i = 0; i < kQTrF4; ++i) ds_write4(tro[i] + so, tb[i]);
+      for (int i = 0; i < kQTrF4; ++i) ds_write4(tro[i] + so, R.tb[i]);
       if constexpr (kTrans) {
-        if (lane < 12) *reinterpret_cast<__attribute__((address_space(3))) float*>(uintptr_t(trs + so)) = trb;
+        if (lane < 12) *reinterpret_cast<__attribute__((address_space(3))) float*>(uintptr_t(trs + so)) = R.trb;
       }
       if (fs < n_full) {
 #pragma unroll
-        for (int i = 0; i < kQF4; ++i) ds_write4(fso[i] + so, rb[i]);
+        for (int i = 0; i < kQF4; ++i) ds_write4(fso[i] + so, R.rb[i]);
       } else {
 #pragma unroll
-        for (int i = 0; i < kQF4; ++i) ds_write4(tso[i] + so, rb[i]);
+        for (int i = 0; i < kQF4; ++i) ds_write4(tso[i] + so, R.rb[i]);
       }
     };
     // The stored data stays live past the next unit's loads (keep_live), so
@@ -517,43 +522,63 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       for (int i = 0; i < kQF4; ++i)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sdata[i]), ro, full ? fvo[i] : tvo[i], soff, 0);
     };
-    // pend*: the units staged and not yet stored (0 = the latest)
+    // pend*: the units staged and not yet stored (0 = the latest);
+    // (q1, s1): the unit after the one to stage next, (q2, s2) the next but one.
     int64_t pend_q[kPairCompute + 1];
     int pend_s[kPairCompute + 1];
     int k = 0;
     bool ok = true;
-    auto stage_next = [&] {  // stage unit k, load unit k + 1
-      stage(s, unsigned(k % kPairSlots));
+    int64_t q1 = qd;
+    int s1 = s;
+    advance(q1, s1);
+    MemRegs RA, RB;
+    RA.trb = RB.trb = 0.f;
+    auto stage_next = [&](MemRegs& R) {  // stage unit k from R, load unit k + 2 into R
+      stage(s, unsigned(k % kPairSlots), R);
       pair_signal(full_flag, k + 1);
 #pragma unroll
       for (int i = kPairCompute; i > 0; --i) pend_q[i] = pend_q[i - 1], pend_s[i] = pend_s[i - 1];
       pend_q[0] = qd;
       pend_s[0] = s;
-      int64_t nq = qd;
-      int ns = s;
-      advance(nq, ns);
-      fetch(nq < n_quads ? nq : qd, nq < n_quads ? ns : s);
+      int64_t q2 = q1;
+      int s2 = s1;
+      advance(q2, s2);
+      fetch(q2 < n_quads ? q2 : qd, q2 < n_quads ? s2 : s, R);
       keep_live();
-      qd = nq;
-      s = ns;
+      qd = q1;
+      s = s1;
+      q1 = q2;
+      s1 = s2;
       ++k;
     };
-    fetch(qd, s);
-    // The first kPairCompute units are staged without a store; then each
-    // iteration stores unit k - kPairCompute (once skinned) BEFORE staging
-    // unit k, so the stage's wait for unit k's loads leaves those stores in
-    // flight on every path into it (hipcc merges the wait counts of the
-    // paths: a path with no store after the loads would force vmcnt(0)).
-    for (int j = 0; j < kPairCompute && qd < n_quads; ++j) stage_next();
-    while (qd < n_quads) {
+    fetch(qd, s, RA);
+    fetch(q1 < n_quads ? q1 : qd, q1 < n_quads ? s1 : s, RB);
+    // The first kPairCompute (= 2) units are staged without a store; then
+    // each step stores unit k - kPairCompute (once skinned) BEFORE staging
+    // unit k, so every path into a stage's wait has the same memory ops
+    // after its loads (hipcc merges the paths' wait counts).
+    // (every pair has at least 2 units: launch_skin_quad sizes the grid so)
+    static_assert(kPairCompute == 2, "the prologue stages one unit per register set");
+    stage_next(RA);
+    stage_next(RB);
+    // Steady state: a fixed count of steps, unrolled by 2 with no exit in
+    // between, so every path into a step's stage has issued the same memory
+    // operations since that set's loads (the other set's loads and two
+    // stores): hipcc's merged wait then leaves the other set in flight.  A
+    // timed-out hand-over only marks the wave broken (later polls are
+    // skipped); the results are then wrong, the kernel still ends.
+    const int64_t n_units = (n_quads * spans - worker + n_workers - 1) / n_workers;  // >= 2
+    auto step = [&](MemRegs& R) {
       const int ku = k - kPairCompute;
-      if (!pair_wait_ge(&sh.done[pair][ku % kPairSlots], ku + 1)) {
-        ok = false;
-        break;
-      }
+      if (ok) ok = pair_wait_ge(&sh.done[pair][ku % kPairSlots], ku + 1);
       store(pend_q[kPairCompute - 1], pend_s[kPairCompute - 1], unsigned(ku % kPairSlots));
-      stage_next();
+      stage_next(R);
+    };
+    for (int64_t i = 2; i + 1 < n_units; i += 2) {
+      step(RA);
+      step(RB);
     }
+    if (n_units % 2 == 1) step(RA);
     // the last min(k, kPairCompute) units
     for (int i = min(k, kPairCompute) - 1; ok && i >= 0; --i) {
       const int ku = k - 1 - i;
@@ -874,7 +899,18 @@ hipError_t launch_skin_quad(const DeviceModel& m, int64_t n, const float* transf
   else launch(skin_dma_kernel<false>);
   return hipGetLastError();
 #elif MANO_QUAD_PAIR
-  blocks = std::min<int64_t>((units + kPairs - 1) / kPairs, cap);
+  // at least 2 units per memory wave (its prologue stages two); a batch too
+  // small for one block of those runs skin_quad_kernel
+  blocks = std::min<int64_t>(units / (2 * kPairs), cap);
+  if (blocks < 1) {
+    auto launch1 = [&](auto kernel) {
+      hipLaunchKernelGGL(kernel, dim3(1), dim3(64 * kQWaves), 0, stream, transforms, m.wfrag16, vposed,
+                         trans, verts, n, m.n_verts, m.n_groups16);
+    };
+    if (trans) launch1(skin_quad_kernel<true>);
+    else launch1(skin_quad_kernel<false>);
+    return hipGetLastError();
+  }
   auto launch = [&](auto kernel) {
     hipLaunchKernelGGL(kernel, dim3(unsigned(blocks)), dim3(64 * kPairWaves), 0, stream, transforms,
                        m.wfrag16, vposed, trans, verts, n, m.n_verts, m.n_groups16);
