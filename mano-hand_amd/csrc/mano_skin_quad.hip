@@ -41,7 +41,6 @@
 
 #include <algorithm>
 #include <cstddef>
-#include <type_traits>
 
 #include "mano_internal.h"
 
@@ -59,7 +58,7 @@ typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
 #endif
 constexpr int kQWaves = MANO_QUAD_WAVES;
 #ifndef MANO_QUAD_ABLATE
-#define MANO_QUAD_ABLATE 0  // diagnostic builds only: 1 = no LBS
+#define MANO_QUAD_ABLATE 0  // diagnostic builds only: 1 = no LBS (skin_quad), 2 = no compute (skin_pair)
 #endif
 constexpr int kQHands = 4;
 constexpr int kQVerts = 64;                                  // vertices per full span
@@ -642,233 +641,6 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
   }
 }
 
-// ---------------------------------------------------------------------------
-// skin_dma_kernel (MANO_QUAD_DMA): skin_pair's roles with the memory wave
-// reduced to LDS-DMA (global_load_lds: v_posed rows, transforms and
-// translations straight into a slot, no registers, no LDS instructions of
-// its own -- so hipcc's conservative waits around LDS-DMA never meet an LDS
-// read) and the store sweep moved to the compute waves.  Slot k % kDSlots:
-// DMA'd by the memory wave (full = k + 1 once landed), skinned in place and
-// streamed out by compute wave k % kPairCompute (freed[slot] = k + 1 once its
-// stage reads are done).  The stage has no row padding (DMA lands lane l at
-// base + 16 l): full-unit rows 192 floats apart, tail rows 3 tail_len floats.
-// ---------------------------------------------------------------------------
-#ifndef MANO_QUAD_DMA
-#define MANO_QUAD_DMA 0
-#endif
-constexpr int kDSlots = 4;
-constexpr int kDmaMaxGroups = 52;
-struct DmaStage {
-  float rows[kQHands * 3 * kQVerts];     // 3,072 B
-  float tr[kQHands * kTransformFloats];  // 3,072 B
-  float trans[64];                       // 12 used; lanes past them land here harmlessly
-};
-struct DmaShared {
-  DmaStage slot[kPairs][kDSlots];
-  int full[kPairs];
-  int freed[kPairs][kDSlots];
-};
-
-template <bool kTrans>
-__global__ __launch_bounds__(64 * kPairWaves, 1) void skin_dma_kernel(
-    const float* __restrict__ transforms, const float* __restrict__ wfrag16,
-    const float* __restrict__ vposed, const float* __restrict__ trans, float* __restrict__ verts,
-    int64_t n, int n_verts, int n_groups) {
-  __shared__ f32x4 w_lds[kDmaMaxGroups * 64];
-  __shared__ DmaShared sh;
-  for (int i = threadIdx.x; i < n_groups * 64; i += 64 * kPairWaves)
-    w_lds[i] = reinterpret_cast<const f32x4*>(wfrag16)[i];
-  if (threadIdx.x < kPairs) sh.full[threadIdx.x] = 0;
-  if (threadIdx.x < kPairs * kDSlots) sh.freed[threadIdx.x / kDSlots][threadIdx.x % kDSlots] = 0;
-  __syncthreads();
-
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int pair = wave & (kPairs - 1);
-  int lane = threadIdx.x & 63;
-  asm volatile("" : "+v"(lane));
-  const int vstride = 3 * n_verts;
-  const int n_full = n_verts / kQVerts;
-  const int n_tail = n_groups - 4 * n_full;
-  const int spans = n_full + (n_tail > 0 ? 1 : 0);
-  const int64_t n_quads = (n + kQHands - 1) / kQHands;
-  const int64_t b = blockIdx.x, nb = gridDim.x;
-  const int64_t blk = (nb % 8) ? b : (b % 8) * (nb / 8) + b / 8;
-  const int64_t worker = blk * kPairs + pair, n_workers = nb * kPairs;
-  const int64_t step_q = n_workers / spans;
-  const int step_s = int(n_workers - step_q * spans);
-  auto advance = [&](int64_t& aq, int& as) {
-    aq += step_q;
-    as += step_s;
-    if (as >= spans) {
-      as -= spans;
-      ++aq;
-    }
-  };
-  const int tail_v0 = min(kQVerts * n_full, n_verts - 16);
-  const int tail_rf4 = 3 * (n_verts - tail_v0) / 4;
-  int64_t qd = worker / spans;
-  int s = int(worker - qd * spans);
-  if (qd >= n_quads) return;
-
-  if (wave < kPairs) {
-    // ---- memory wave: DMA only ----
-    constexpr int kDmaOps = 6 + (kTrans ? 1 : 0);  // LDS-DMA instructions per unit
-    auto dma = [&](int64_t fq, int fs, int slot) {
-      DmaStage& st = sh.slot[pair][slot];
-      const int64_t h0 = fq * kQHands;
-      const int last = int(n - h0 < kQHands ? n - h0 : kQHands) - 1;
-      const bool full = fs < n_full;
-      const int rf4 = full ? kQRowF4 : tail_rf4;
-      const float* src = vposed + h0 * vstride + 3 * (full ? kQVerts * fs : tail_v0);
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int idx = min(64 * i + lane, kQHands * rf4 - 1);
-        const int row = min(idx / rf4, last);
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(src + unsigned(row * vstride + 4 * (idx % rf4))),
-            (__attribute__((address_space(3))) void*)(st.rows + 256 * i), 16, 0, 0);
-      }
-      const float* tsrc = transforms + h0 * kTransformFloats;
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int idx = 64 * i + lane;
-        const int h = min(idx / kQTrF4PerHand, last);
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(tsrc + unsigned(h * kTransformFloats + 4 * (idx % kQTrF4PerHand))),
-            (__attribute__((address_space(3))) void*)(st.tr + 256 * i), 16, 0, 0);
-      }
-      if constexpr (kTrans) {
-        const int l = min(lane, 11);
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(trans + h0 * 3 + unsigned(min(l / 3, last) * 3 + l % 3)),
-            (__attribute__((address_space(3))) void*)st.trans, 4, 0, 0);
-      }
-    };
-    // unit k is DMA'd one unit ahead of its hand-over: full = k + 1 once its
-    // kDmaOps have landed, i.e. once at most the next unit's are in flight
-    int k = 0;
-    dma(qd, s, 0);
-    int64_t q1 = qd;
-    int s1 = s;
-    advance(q1, s1);
-    while (true) {
-      const bool more = q1 < n_quads;
-      if (more) {
-        // slot of unit k + 1 free?  (unit k + 1 - kDSlots streamed out)
-        const int kn = k + 1;
-        if (kn >= kDSlots && !pair_wait_ge(&sh.freed[pair][kn % kDSlots], kn - kDSlots + 1)) return;
-        dma(q1, s1, kn % kDSlots);
-        if constexpr (kDmaOps == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      pair_signal(&sh.full[pair], k + 1);
-      if (!more) break;
-      ++k;
-      qd = q1;
-      s = s1;
-      advance(q1, s1);
-    }
-    return;
-  }
-
-  // ---- compute waves ----
-  const int q = lane >> 4, v = lane & 15;
-  int hh[3], cc[3], a_off[3];
-#pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    const int m0 = 16 * t + 4 * q, m = 16 * t + v;
-    hh[t] = m0 / 12;
-    cc[t] = (m0 % 12) / 4;
-    a_off[t] = (m / 12) * kTransformFloats + 12 * q + m % 12;
-  }
-  const int cw = (wave - kPairs) / kPairs;
-  for (int i = 0; i < cw; ++i) advance(qd, s);
-  f32x4 sdata[3] = {};
-  for (int k = cw; qd < n_quads; k += kPairCompute) {
-    if (!pair_wait_ge(&sh.full[pair], k + 1)) return;
-    DmaStage& st = sh.slot[pair][k % kDSlots];
-    const int64_t h0 = qd * kQHands;
-    const int last = int(n - h0 < kQHands ? n - h0 : kQHands) - 1;
-    const bool full = s < n_full;
-    const int rs = full ? 3 * kQVerts : 4 * tail_rf4;  // stage row stride (floats)
-    float a[3][4], tr3[3];
-#pragma unroll
-    for (int t = 0; t < 3; ++t) {
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) a[t][kk] = st.tr[a_off[t] + 4 * 12 * kk];
-      tr3[t] = kTrans ? st.trans[3 * hh[t] + cc[t]] : 0.f;
-    }
-    // skin in place (every point read before any output lands)
-    {
-      int G[4], lv[4], NG;
-      if (full) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) G[g] = 4 * s + g, lv[g] = 16 * g;
-        NG = 4;
-      } else {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          G[g] = 4 * n_full + min(g, n_tail - 1);
-          lv[g] = min(16 * G[g], n_verts - 16) - tail_v0;
-        }
-        NG = n_tail == 1 ? 1 : 4;
-      }
-      auto run = [&](auto ng_tag) {
-        constexpr int NGc = decltype(ng_tag)::value;
-        f32x4 wf[NGc];
-        float p[NGc][3][3];
-#pragma unroll
-        for (int g = 0; g < NGc; ++g) wf[g] = w_lds[G[g] * 64 + lane];
-#pragma unroll
-        for (int g = 0; g < NGc; ++g)
-#pragma unroll
-          for (int t = 0; t < 3; ++t)
-#pragma unroll
-            for (int c = 0; c < 3; ++c) p[g][t][c] = st.rows[hh[t] * rs + 3 * (lv[g] + v) + c];
-        f32x4 T[NGc][3];
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-          for (int g = 0; g < NGc; ++g)
-#pragma unroll
-            for (int t = 0; t < 3; ++t)
-              T[g][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][kk], wf[g][kk], kk == 0 ? f32x4{} : T[g][t], 0, 0, 0);
-#pragma unroll
-        for (int g = 0; g < NGc; ++g)
-#pragma unroll
-          for (int t = 0; t < 3; ++t) {
-            float o = T[g][t][3];
-            o = fmaf(T[g][t][2], p[g][t][2], o);
-            o = fmaf(T[g][t][1], p[g][t][1], o);
-            o = fmaf(T[g][t][0], p[g][t][0], o);
-            if constexpr (kTrans) o = o + tr3[t];
-            st.rows[hh[t] * rs + 3 * (lv[g] + v) + cc[t]] = o;
-          }
-      };
-      if (NG == 4) run(std::integral_constant<int, 4>{});
-      else run(std::integral_constant<int, 1>{});
-    }
-    // stream the skinned rows out (the DMA's flat sweep in reverse)
-    {
-      const int rf4 = full ? kQRowF4 : tail_rf4;
-      float* dst = verts + h0 * vstride + 3 * (full ? kQVerts * s : tail_v0);
-#pragma unroll
-      for (int i = 0; i < 3; ++i) sdata[i] = *reinterpret_cast<const f32x4*>(st.rows + 4 * min(64 * i + lane, kQHands * rf4 - 1));
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int idx = min(64 * i + lane, kQHands * rf4 - 1);
-        const int row = min(idx / rf4, last);
-        *reinterpret_cast<f32x4u*>(dst + unsigned(row * vstride + 4 * (idx % rf4))) = sdata[i];
-      }
-    }
-    pair_signal(&sh.freed[pair][k % kDSlots], k + 1);  // (waits for the stage reads)
-#pragma unroll
-    for (int i = 0; i < kPairCompute; ++i) advance(qd, s);
-  }
-}
-
 }  // namespace
 
 bool skin_quad_supported(const DeviceModel& m) {
@@ -889,16 +661,7 @@ hipError_t launch_skin_quad(const DeviceModel& m, int64_t n, const float* transf
   int64_t blocks = (units + kQWaves - 1) / kQWaves;
   const int64_t cap = m.n_cu > 0 ? m.n_cu : 1;
   if (blocks > cap) blocks = cap;
-#if MANO_QUAD_DMA
-  blocks = std::min<int64_t>((units + kPairs - 1) / kPairs, cap);
-  auto launch = [&](auto kernel) {
-    hipLaunchKernelGGL(kernel, dim3(unsigned(blocks)), dim3(64 * kPairWaves), 0, stream, transforms,
-                       m.wfrag16, vposed, trans, verts, n, m.n_verts, m.n_groups16);
-  };
-  if (trans) launch(skin_dma_kernel<true>);
-  else launch(skin_dma_kernel<false>);
-  return hipGetLastError();
-#elif MANO_QUAD_PAIR
+#if MANO_QUAD_PAIR
   // at least 2 units per memory wave (its prologue stages two); a batch too
   // small for one block of those runs skin_quad_kernel
   blocks = std::min<int64_t>(units / (2 * kPairs), cap);
