@@ -236,6 +236,24 @@ def test_root_rotation_equivariance(engine, dev, params):
     assert np.abs(turned["verts"] - expect).max() <= 2 * TOL_M
 
 
+def test_scan_pose_source(engine, dev, params):
+    """The realistic pose source of data_explore.py:12-15: the reference's own
+    dump_scans() output (tests/golden/mano_reference_scans.npz, 73 captured
+    poses; the right hand mirrored by [1, -1, -1]) with a zero root, shared
+    betas and per-hand betas, through the batched forward vs the oracle."""
+    import os
+    from conftest import GOLDEN
+    from mano_amd import scans_to_pose
+    with np.load(os.path.join(GOLDEN, "mano_reference_scans.npz"), allow_pickle=False) as z:
+        pose = scans_to_pose(z["axangles"])
+    B = pose.shape[0]
+    rng = np.random.default_rng(73)
+    for betas in (np.zeros((B, 10)), rng.normal(0, 1, (B, 10))):
+        out = run(engine, dev, betas, pose)
+        ref = mano_oracle.forward(params, betas, pose)
+        assert_close(out, ref, "scan poses")
+
+
 def test_empty_batch(engine, dev):
     out = engine.forward(torch.empty((0, 10), device=dev), torch.empty((0, 16, 3), device=dev))
     assert out["verts"].shape == (0, 778, 3)
