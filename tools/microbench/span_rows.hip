@@ -22,7 +22,9 @@ struct Unit {
   static_assert(R * kRowF4 % 64 == 0, "unit must be whole wave sweeps");
 };
 
-template <int R, int V, int B>
+// ORDER 0: grid-stride over (tile, span) units; 1: a wave takes tiles
+// w, w + nw, ... and sweeps all spans of each (tile-major per wave).
+template <int R, int V, int B, int ORDER = 0>
 __global__ __launch_bounds__(256, B) void span_rows(const float* __restrict__ in, float* __restrict__ out,
                                                     long n) {
   using U = Unit<R, V>;
@@ -42,12 +44,19 @@ __global__ __launch_bounds__(256, B) void span_rows(const float* __restrict__ in
       v[i] = *reinterpret_cast<const f32x4u*>(src + row * VS + 4 * c4);
     }
   };
-  if (w < units) load(w);
-  for (long u = w; u < units; u += nw) {
+  auto next = [&](long u) {
+    if (ORDER == 0) return u + nw;
+    const long t = u / U::kSpans;
+    const int s = int(u - t * U::kSpans);
+    return s + 1 < U::kSpans ? u + 1 : (t + nw) * U::kSpans;
+  };
+  const long u0 = ORDER == 0 ? w : w * U::kSpans;
+  if (u0 < units) load(u0);
+  for (long u = u0; u < units; u = next(u)) {
     f32x4u c[U::kF4];
 #pragma unroll
     for (int i = 0; i < U::kF4; ++i) c[i] = v[i];
-    if (u + nw < units) load(u + nw);
+    if (next(u) < units) load(next(u));
     const long t = u / U::kSpans;
     const int s = int(u - t * U::kSpans);
     float* dst = out + t * R * VS + 3 * V * s;
@@ -63,23 +72,23 @@ __global__ __launch_bounds__(256) void copy16(const f32x4* __restrict__ in, f32x
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += gridDim.x * 256L) out[i] = in[i] * 2.f;
 }
 
-template <int R, int V, int B>
+template <int R, int V, int B, int ORDER = 0>
 void run(const float* a, float* o, long n, int n_cu) {
   using U = Unit<R, V>;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (int i = 0; i < 50; ++i) hipLaunchKernelGGL((span_rows<R, V, B>), dim3(n_cu * B), dim3(256), 0, 0, a, o, n);
+  for (int i = 0; i < 50; ++i) hipLaunchKernelGGL((span_rows<R, V, B, ORDER>), dim3(n_cu * B), dim3(256), 0, 0, a, o, n);
   CK(hipEventRecord(e0));
   const int reps = 100;
-  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((span_rows<R, V, B>), dim3(n_cu * B), dim3(256), 0, 0, a, o, n);
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((span_rows<R, V, B, ORDER>), dim3(n_cu * B), dim3(256), 0, 0, a, o, n);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   float ms = 0;
   CK(hipEventElapsedTime(&ms, e0, e1));
   ms /= reps;
   const double bytes = 2.0 * double(n) * U::kSpans * V * 12;
-  printf("R=%2d V=%3d blocks/CU=%d  f4/lane=%2d  %.4f ms  %.0f GB/s  (x %.4f = full-row ms)\n", R, V, B, U::kF4, ms,
+  printf("%s R=%2d V=%3d blocks/CU=%d  f4/lane=%2d  %.4f ms  %.0f GB/s  (x %.4f = full-row ms)\n", ORDER ? "tile-major " : "grid-stride", R, V, B, U::kF4, ms,
          bytes / ms * 1e-6, ms * NV / (U::kSpans * V));
 }
 
@@ -123,6 +132,10 @@ int main() {
     run<1, 256, 2>(a, o, n, n_cu);
     run<16, 16, 1>(a, o, n, n_cu);
     run<16, 16, 2>(a, o, n, n_cu);
+    run<4, 64, 1, 1>(a, o, n, n_cu);
+    run<4, 64, 2, 1>(a, o, n, n_cu);
+    run<16, 64, 1, 1>(a, o, n, n_cu);
+    run<8, 64, 1, 1>(a, o, n, n_cu);
   }
   return 0;
 }
