@@ -590,6 +590,24 @@ __device__ __forceinline__ void store_out(float* dst, f32x3 v) {
 // group in slot q), so the barrier after tile t waits for tile t + 1's DMA
 // only: it was issued before the previous group's output stores, which stay
 // in flight (counted vmcnt, below).
+// Diagnostic build only (MANO_BS_STAMP=1, tools/debug/bs_stamps.py): per wave
+// the shader clock and the 100-MHz real-time clock at entry and exit, the
+// hardware ids and the units it ran, read back by mano_debug_bs_stamps().
+#ifndef MANO_BS_STAMP
+#define MANO_BS_STAMP 0
+#endif
+#if MANO_BS_STAMP
+constexpr int kStampWaves = 4096;
+__device__ unsigned long long g_bs_stamps[kStampWaves * 8];
+__device__ __forceinline__ void bs_stamp(int slot, unsigned long long v) {
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0 && w < kStampWaves) {
+    volatile unsigned long long* p = g_bs_stamps + w * 8 + slot;
+    *p = v;
+  }
+}
+#endif
+
 template <bool kTrans, bool kVposed>
 __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
     const float* __restrict__ features, const float* __restrict__ transforms,
@@ -614,8 +632,19 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
   const int64_t n_quads = (nt16 + 3) / 4;
   int64_t u, u_end;
   unit_range(n_quads * n_groups, blockIdx.x, gridDim.x, u, u_end);
+#if MANO_BS_STAMP
+  bs_stamp(0, __builtin_amdgcn_s_memtime());
+  bs_stamp(2, __builtin_amdgcn_s_memrealtime());
+  bs_stamp(4, (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                  ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32));
+  bs_stamp(5, (unsigned long long)(u_end - u));
+  int n_ranges = 0;
+#endif
 
   while (u < u_end) {
+#if MANO_BS_STAMP
+    ++n_ranges;
+#endif
     const int64_t quad = u / n_groups;
     const int g0 = int(u - quad * n_groups);
     const int g1 = int(n_groups - g0 < u_end - u ? n_groups : g0 + (u_end - u));
@@ -785,6 +814,11 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
       prio_down<kStorePrio>();
     }
   }
+#if MANO_BS_STAMP
+  bs_stamp(1, __builtin_amdgcn_s_memtime());
+  bs_stamp(3, __builtin_amdgcn_s_memrealtime());
+  bs_stamp(6, (unsigned long long)n_ranges);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1263,6 +1297,16 @@ hipError_t launch_skin(const DeviceModel& m, int64_t n, const float* transforms,
   else launch(skin_span_kernel<false>);
   return hipGetLastError();
 }
+
+#if MANO_BS_STAMP
+}  // namespace mano
+extern "C" int mano_debug_bs_stamps(unsigned long long* host, int count) {
+  if (count > mano::kStampWaves * 8) count = mano::kStampWaves * 8;
+  return int(hipMemcpyFromSymbol(host, HIP_SYMBOL(mano::g_bs_stamps), size_t(count) * 8, 0,
+                                 hipMemcpyDeviceToHost));
+}
+namespace mano {
+#endif
 
 hipError_t launch_pose_from_pca(const DeviceModel& m, int64_t n, const float* pca, int n_comps,
                                 int64_t pca_stride, const float* rot, int64_t rot_stride,

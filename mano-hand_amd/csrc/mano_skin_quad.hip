@@ -343,6 +343,12 @@ __global__ __launch_bounds__(64 * kQWaves, 1) void skin_quad_kernel(
 #ifndef MANO_QUAD_PAIR_PRIO
 #define MANO_QUAD_PAIR_PRIO 0  // issue priority of the memory waves
 #endif
+#ifndef MANO_PAIR_NT
+#define MANO_PAIR_NT 0  // nontemporal memory-wave accesses: 1 = v_posed loads, 2 = verts stores, 4 = transforms loads
+#endif
+constexpr int kPairNtRows = (MANO_PAIR_NT & 1) ? 2 : 0;  // buffer cache-policy aux: 2 = nt on gfx950
+constexpr int kPairNtStores = (MANO_PAIR_NT & 2) ? 2 : 0;
+constexpr int kPairNtTr = (MANO_PAIR_NT & 4) ? 2 : 0;
 constexpr int kPairs = 4;
 constexpr int kPairCompute = MANO_QUAD_PAIR_COMPUTE;
 constexpr int kPairSlots = 2 * kPairCompute;
@@ -364,13 +370,26 @@ __device__ __forceinline__ unsigned lds_addr(const int* p) {
 }
 // Bounded: false after ~2^20 polls (tens of ms), and the caller then stops
 // -- a lost hand-over ends the kernel with wrong results, never hangs it.
+#ifndef MANO_PAIR_STAGE_FIRST
+#define MANO_PAIR_STAGE_FIRST 1  // memory step order: stage k, store k - 2, load k + 2 (0: store k - 2 first)
+#endif
+#ifndef MANO_PAIR_EXTRA_VALU
+#define MANO_PAIR_EXTRA_VALU 0
+#endif
+#ifndef MANO_PAIR_SLEEP_MEM
+#define MANO_PAIR_SLEEP_MEM 1  // s_sleep between the memory wave's polls (0 = none)
+#endif
+#ifndef MANO_PAIR_SLEEP_CMP
+#define MANO_PAIR_SLEEP_CMP 1  // s_sleep between a compute wave's polls
+#endif
+template <int kSleep = 1>
 __device__ __forceinline__ bool pair_wait_ge(const int* flag, int target) {
   const unsigned a = lds_addr(flag);
   for (int it = 0; it < (1 << 20); ++it) {
     int x;
     asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(x) : "v"(a) : "memory");
     if (__builtin_amdgcn_readfirstlane(x) >= target) return true;
-    __builtin_amdgcn_s_sleep(1);
+    if constexpr (kSleep > 0) __builtin_amdgcn_s_sleep(kSleep);
   }
   return false;
 }
@@ -380,6 +399,38 @@ __device__ __forceinline__ void pair_signal(int* flag, int value) {
 }
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// Diagnostic build only (MANO_PAIR_STAMP=1, tools/debug/pair_stamps.py): per
+// wave the shader-clock cycles from entry to exit, the cycles spent in the
+// hand-over polls and the units handled, read back by mano_debug_pair_stamps().
+#ifndef MANO_PAIR_STAMP
+#define MANO_PAIR_STAMP 0
+#endif
+#if MANO_PAIR_STAMP
+constexpr int kPairStampWaves = 256 * 12;
+__device__ unsigned long long g_pair_stamps[kPairStampWaves * 4];
+struct PairStamp {
+  unsigned long long t0, wait = 0, units = 0;
+  __device__ PairStamp() : t0(__builtin_amdgcn_s_memtime()) {}
+  __device__ void done(int wave) {
+    const int w = blockIdx.x * 12 + wave;
+    if ((threadIdx.x & 63) == 0 && w < kPairStampWaves) {
+      volatile unsigned long long* p = g_pair_stamps + w * 4;
+      p[0] = __builtin_amdgcn_s_memtime() - t0;
+      p[1] = wait;
+      p[2] = units;
+      p[3] = 1;
+    }
+  }
+};
+#define PAIR_TIMED(expr, st) ({ const unsigned long long _t = __builtin_amdgcn_s_memtime(); auto _r = (expr); st.wait += __builtin_amdgcn_s_memtime() - _t; _r; })
+#else
+struct PairStamp {
+  unsigned long long units = 0;
+  __device__ void done(int) {}
+};
+#define PAIR_TIMED(expr, st) (expr)
+#endif
 
 template <bool kTrans>
 __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
@@ -423,6 +474,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
   int s = int(worker - qd * spans);
   if (qd >= n_quads) return;
 
+  PairStamp stamp;
   if (is_mem) {
     if (MANO_QUAD_PAIR_PRIO) __builtin_amdgcn_s_setprio(MANO_QUAD_PAIR_PRIO);
     // The memory wave shares its SIMD with the compute waves' f32 MFMAs,
@@ -467,7 +519,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       const auto rt = rsrc(transforms + h0 * kTransformFloats, int64_t(valid) * kTransformFloats);
 #pragma unroll
       for (int i = 0; i < kQTrF4; ++i)
-        R.tb[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * (64 * i + lane), 0, 0));
+        R.tb[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * (64 * i + lane), 0, kPairNtTr));
       if constexpr (kTrans) {
         const auto rr = rsrc(trans + h0 * 3, int64_t(valid) * 3);
         R.trb = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, 4 * lane, 0, 0));
@@ -476,7 +528,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       const int soff = 4 * 3 * (full ? kQVerts * fs : tail_v0);
 #pragma unroll
       for (int i = 0; i < kQF4; ++i)
-        R.rb[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, full ? fvo[i] : tvo[i], soff, 0));
+        R.rb[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, full ? fvo[i] : tvo[i], soff, kPairNtRows));
     };
     auto ds_write4 = [](unsigned addr, const f32x4& v) {
       *reinterpret_cast<__attribute__((address_space(3))) f32x4*>(uintptr_t(addr)) = v;
@@ -519,7 +571,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       for (int i = 0; i < kQF4; ++i) sdata[i] = ds_read4((full ? fso[i] : tso[i]) + so);
 #pragma unroll
       for (int i = 0; i < kQF4; ++i)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sdata[i]), ro, full ? fvo[i] : tvo[i], soff, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sdata[i]), ro, full ? fvo[i] : tvo[i], soff, kPairNtStores);
     };
     // pend*: the units staged and not yet stored (0 = the latest);
     // (q1, s1): the unit after the one to stage next, (q2, s2) the next but one.
@@ -532,16 +584,49 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     advance(q1, s1);
     MemRegs RA, RB;
     RA.trb = RB.trb = 0.f;
-    auto stage_next = [&](MemRegs& R) {  // stage unit k from R, load unit k + 2 into R
+#if MANO_PAIR_STAGE_FIRST
+    // A prologue step's stand-in for store(k - 2): the same 3 buffer stores
+    // through a resource of num_records 0 (every lane out of range: dropped),
+    // so prologue and steady steps issue the same memory operations.
+    auto dummy_store = [&] {
+      const auto ro = rsrc(verts, 0);
+#pragma unroll
+      for (int i = 0; i < kQF4; ++i)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sdata[i]), ro, fvo[i], 0, kPairNtStores);
+    };
+#endif
+    // Stage unit k from R, then (MANO_PAIR_STAGE_FIRST) store unit k - 2 once
+    // skinned, then load unit k + 2 into R.
+    auto stage_next = [&](MemRegs& R, bool store_prev) {
       stage(s, unsigned(k % kPairSlots), R);
       pair_signal(full_flag, k + 1);
 #pragma unroll
       for (int i = kPairCompute; i > 0; --i) pend_q[i] = pend_q[i - 1], pend_s[i] = pend_s[i - 1];
       pend_q[0] = qd;
       pend_s[0] = s;
+#if MANO_PAIR_STAGE_FIRST
+      if (store_prev) {
+        const int ku = k - kPairCompute;
+        if (ok) ok = PAIR_TIMED(pair_wait_ge<MANO_PAIR_SLEEP_MEM>(&sh.done[pair][ku % kPairSlots], ku + 1), stamp);
+        ++stamp.units;
+        store(pend_q[kPairCompute], pend_s[kPairCompute], unsigned(ku % kPairSlots));
+      } else {
+        dummy_store();
+      }
+#else
+      (void)store_prev;
+#endif
       int64_t q2 = q1;
       int s2 = s1;
       advance(q2, s2);
+#if MANO_PAIR_EXTRA_VALU  // diagnostic: N dependent VALU ops per unit in the memory wave
+      {
+        int d = lane;
+#pragma unroll
+        for (int e = 0; e < MANO_PAIR_EXTRA_VALU; ++e) asm volatile("v_add_u32 %0, 1, %0" : "+v"(d));
+        asm volatile("" ::"v"(d));
+      }
+#endif
       fetch(q2 < n_quads ? q2 : qd, q2 < n_quads ? s2 : s, R);
       keep_live();
       qd = q1;
@@ -558,8 +643,8 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     // after its loads (hipcc merges the paths' wait counts).
     // (every pair has at least 2 units: launch_skin_quad sizes the grid so)
     static_assert(kPairCompute == 2, "the prologue stages one unit per register set");
-    stage_next(RA);
-    stage_next(RB);
+    stage_next(RA, false);
+    stage_next(RB, false);
     // Steady state: a fixed count of steps, unrolled by 2 with no exit in
     // between, so every path into a step's stage has issued the same memory
     // operations since that set's loads (the other set's loads and two
@@ -568,10 +653,15 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     // skipped); the results are then wrong, the kernel still ends.
     const int64_t n_units = (n_quads * spans - worker + n_workers - 1) / n_workers;  // >= 2
     auto step = [&](MemRegs& R) {
+#if MANO_PAIR_STAGE_FIRST
+      stage_next(R, true);
+#else
       const int ku = k - kPairCompute;
-      if (ok) ok = pair_wait_ge(&sh.done[pair][ku % kPairSlots], ku + 1);
+      if (ok) ok = PAIR_TIMED(pair_wait_ge<MANO_PAIR_SLEEP_MEM>(&sh.done[pair][ku % kPairSlots], ku + 1), stamp);
+      ++stamp.units;
       store(pend_q[kPairCompute - 1], pend_s[kPairCompute - 1], unsigned(ku % kPairSlots));
-      stage_next(R);
+      stage_next(R, false);
+#endif
     };
     for (int64_t i = 2; i + 1 < n_units; i += 2) {
       step(RA);
@@ -581,9 +671,10 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     // the last min(k, kPairCompute) units
     for (int i = min(k, kPairCompute) - 1; ok && i >= 0; --i) {
       const int ku = k - 1 - i;
-      if (!pair_wait_ge(&sh.done[pair][ku % kPairSlots], ku + 1)) break;
+      if (!pair_wait_ge<MANO_PAIR_SLEEP_MEM>(&sh.done[pair][ku % kPairSlots], ku + 1)) break;
       store(pend_q[i], pend_s[i], unsigned(ku % kPairSlots));
     }
+    stamp.done(wave);
     return;
   }
 
@@ -601,7 +692,8 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
   const int cw = (wave - kPairs) / kPairs;
   for (int i = 0; i < cw; ++i) advance(qd, s);
   for (int k = cw; qd < n_quads; k += kPairCompute) {
-    if (!pair_wait_ge(full_flag, k + 1)) return;
+    if (!PAIR_TIMED(pair_wait_ge<MANO_PAIR_SLEEP_CMP>(full_flag, k + 1), stamp)) return;
+    ++stamp.units;
     QuadStage& st = sh.slot[pair][k % kPairSlots];
     if (MANO_QUAD_ABLATE & 2) {  // diagnostic: no compute (the memory waves alone)
       pair_signal(&sh.done[pair][k % kPairSlots], k + 1);
@@ -639,9 +731,20 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
 #pragma unroll
     for (int i = 0; i < kPairCompute; ++i) advance(qd, s);
   }
+  stamp.done(wave);
 }
 
 }  // namespace
+
+#if MANO_PAIR_STAMP
+}  // namespace mano
+extern "C" int mano_debug_pair_stamps(unsigned long long* host, int count) {
+  if (count > mano::kPairStampWaves * 4) count = mano::kPairStampWaves * 4;
+  return int(hipMemcpyFromSymbol(host, HIP_SYMBOL(mano::g_pair_stamps), size_t(count) * 8, 0,
+                                 hipMemcpyDeviceToHost));
+}
+namespace mano {
+#endif
 
 bool skin_quad_supported(const DeviceModel& m) {
 #if MANO_QUAD_PAIR

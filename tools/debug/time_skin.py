@@ -19,7 +19,7 @@ g = torch.Generator(device=dev).manual_seed(3)
 betas = torch.randn((B, 10), generator=g, device=dev)
 pose = 0.5 * torch.randn((B, 16, 3), generator=g, device=dev)
 trans = torch.rand((B, 3), generator=g, device=dev)
-for prec in ("fp32", "f16x3"):
+for prec in os.environ.get("PRECS", "fp32,f16x3").split(","):
     m = ManoHip(synthetic_params(0), device=0, precision=prec)
     fused = m.forward(betas, pose, trans, rest_verts=True)
     vp = fused["rest_verts"].clone()
