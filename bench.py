@@ -336,6 +336,18 @@ def main(argv=None):
         for path in ("forward", "api", "unfused"):
             if path != args.path:
                 time_path(path, ms)
+        # The standalone LBS back to back (each launch after another LBS
+        # launch, as rocprof's kernel average sees it); in the unfused path
+        # it follows the blend GEMM's 612 MB of freshly written v_posed.
+        for _ in range(20):
+            model.stage_skin(B, verts, trans=trans)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(50)]
+        for e0, e1 in evs:
+            e0.record(stream)
+            model.stage_skin(B, verts, trans=trans)
+            e1.record(stream)
+        torch.cuda.synchronize()
+        ms["skin_back_to_back"] = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
         model.set_precision(other)
         for path in ("forward", "unfused"):
             time_path(path, ms_other)
@@ -382,6 +394,10 @@ def main(argv=None):
                            "ms": ms["skin"], "bound": "hbm",
                            "achieved_GBs": a, "frac": a / PEAK_HBM_GBS,
                            "bytes_per_hand": SKIN_BYTES_PER_HAND}
+        if "skin_back_to_back" in ms:
+            b2b = ms["skin_back_to_back"]
+            kernels["skin"].update({"ms_back_to_back": b2b, "achieved_GBs_back_to_back": gbs(SKIN_BYTES_PER_HAND, b2b),
+                                    "frac_back_to_back": gbs(SKIN_BYTES_PER_HAND, b2b) / PEAK_HBM_GBS})
     for k, v in kernels.items():
         v["in_timed_path"] = k in in_path
         v["precision"] = args.precision

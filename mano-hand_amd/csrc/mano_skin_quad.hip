@@ -23,12 +23,12 @@
 //
 // Two kernels share these units and this arithmetic:
 //   skin_pair_kernel (default): per SIMD one memory wave (v_posed rows and
-//     the 4 hands' transforms -> an LDS stage slot; skinned slot -> verts)
-//     and two compute waves (slot -> MFMA -> slot, alternate units), four
-//     slots per memory wave handed over through LDS counters -- the HBM
+//     the 4 hands' transforms LDS-DMA'd into a stage slot; skinned slot ->
+//     verts) and two compute waves (slot -> MFMA -> slot, alternate units),
+//     four slots per memory wave handed over through LDS counters -- the HBM
 //     stream runs at one streaming wave per SIMD, the span_rows optimum,
-//     with the MFMA work beside it.  0.274-0.276 ms at 65,536 hands (trans),
-//     58 % of 8 TB/s (tools/debug/time_skin.py).
+//     with the MFMA work beside it.  0.252-0.258 ms at 65,536 hands (trans),
+//     61-63 % of 8 TB/s (tools/debug/time_skin.py).
 //   skin_quad_kernel (MANO_QUAD_PAIR=0): every wave does both roles for its
 //     own units, 2 waves per SIMD: 0.286-0.291 ms.
 // Per block (one per CU): every group's W fragment resident in LDS (n_groups16
@@ -94,13 +94,10 @@ __device__ __forceinline__ void wave_sync() {
 // NG groups (G[0..NG)): the full units and a 1-group tail skip the
 // duplicates a multi-group tail needs.
 template <bool kTrans, int NG = 4>
-__device__ __forceinline__ void skin_unit4(QuadStage& st, const f32x4* w_lds, const float (&a)[3][4],
-                                           const float (&tr3)[3], const int (&G)[4], const int (&lv)[4],
-                                           const int (&hh)[3], const int (&cc)[3], int v, int lane) {
-  f32x4 wf[NG];
+__device__ __forceinline__ void skin_unit4_w(QuadStage& st, const f32x4 (&wf)[4], const float (&a)[3][4],
+                                             const float (&tr3)[3], const int (&lv)[4], const int (&hh)[3],
+                                             const int (&cc)[3], int v) {
   float p[NG][3][3];
-#pragma unroll
-  for (int g = 0; g < NG; ++g) wf[g] = w_lds[G[g] * 64 + lane];
 #pragma unroll
   for (int g = 0; g < NG; ++g)
 #pragma unroll
@@ -126,6 +123,17 @@ __device__ __forceinline__ void skin_unit4(QuadStage& st, const f32x4* w_lds, co
       if constexpr (kTrans) o = o + tr3[t];
       st.rows[hh[t] * kQStride + 3 * (lv[g] + v) + cc[t]] = o;
     }
+}
+
+// skin_unit4_w with the groups' W fragments read from the block's LDS copy.
+template <bool kTrans, int NG = 4>
+__device__ __forceinline__ void skin_unit4(QuadStage& st, const f32x4* w_lds, const float (&a)[3][4],
+                                           const float (&tr3)[3], const int (&G)[4], const int (&lv)[4],
+                                           const int (&hh)[3], const int (&cc)[3], int v, int lane) {
+  f32x4 wf[4];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) wf[g] = w_lds[G[g] * 64 + lane];
+  skin_unit4_w<kTrans, NG>(st, wf, a, tr3, lv, hh, cc, v);
 }
 
 template <bool kTrans>
@@ -325,13 +333,16 @@ __global__ __launch_bounds__(64 * kQWaves, 1) void skin_quad_kernel(
 
 // ---------------------------------------------------------------------------
 // skin_pair_kernel: skin_quad's units with the roles split per SIMD.  Memory
-// wave w (0..3) stages unit k into slot k % kPairSlots, signals full = k + 1,
-// loads unit k + 1, then stores unit k - kPairCompute once its slot's done
-// counter says it is skinned; compute wave c of pair w (wave 4 + 4c + w,
-// same SIMD) skins units c, c + kPairCompute, ... in place and sets the
-// slot's done counter.  Measured (65,536 hands): one compute wave per
-// memory wave 0.335-0.374 ms (the compute side is the bottleneck), two
-// 0.274-0.276, the memory waves alone (no LBS) 0.241-0.265.
+// wave w (0..3), step k: once unit k's DMA into slot k % kPairSlots has
+// landed it signals full = k + 1, then stores unit k - kPairCompute once that
+// slot's done counter says it is skinned, then DMAs unit k + 2 into the slot
+// just read out; compute wave c of pair w (wave 4 + 4c + w, same SIMD) skins
+// units c, c + kPairCompute, ... in place and sets the slot's done counter.
+// Staging unit k BEFORE waiting for unit k - 2 gives each unit two memory
+// steps of compute (the poll stamps).  Measured (65,536
+// hands, trans): 0.252-0.258 ms; register staging instead of LDS-DMA 0.262;
+// the wait before the stage 0.275; one compute wave per memory wave
+// 0.335-0.374; the memory waves alone (no LBS) 0.241-0.265.
 // ---------------------------------------------------------------------------
 #ifndef MANO_QUAD_PAIR
 #define MANO_QUAD_PAIR 1  // the default standalone LBS; 0 = skin_quad_kernel
@@ -351,7 +362,11 @@ constexpr int kPairNtStores = (MANO_PAIR_NT & 2) ? 2 : 0;
 constexpr int kPairNtTr = (MANO_PAIR_NT & 4) ? 2 : 0;
 constexpr int kPairs = 4;
 constexpr int kPairCompute = MANO_QUAD_PAIR_COMPUTE;
-constexpr int kPairSlots = 2 * kPairCompute;
+#ifndef MANO_PAIR_SLOTS
+#define MANO_PAIR_SLOTS 4  // stage slots per memory wave (LDS-DMA path: units k + 1 .. k + SLOTS - 2 in flight)
+#endif
+constexpr int kPairSlots = MANO_PAIR_SLOTS;
+
 constexpr int kPairWaves = kPairs * (1 + kPairCompute);
 constexpr int kPairMaxGroups = 52;  // W in LDS beside the slots: V <= 832
 
@@ -370,6 +385,9 @@ __device__ __forceinline__ unsigned lds_addr(const int* p) {
 }
 // Bounded: false after ~2^20 polls (tens of ms), and the caller then stops
 // -- a lost hand-over ends the kernel with wrong results, never hangs it.
+#ifndef MANO_PAIR_DMA
+#define MANO_PAIR_DMA 1  // memory wave loads with LDS-DMA (no register staging; 0: buffer loads into registers, then ds_write)
+#endif
 #ifndef MANO_PAIR_STAGE_FIRST
 #define MANO_PAIR_STAGE_FIRST 1  // memory step order: stage k, store k - 2, load k + 2 (0: store k - 2 first)
 #endif
@@ -400,6 +418,19 @@ __device__ __forceinline__ void pair_signal(int* flag, int value) {
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
+// LDS-DMA buffer loads (device-only helpers: the host pass of a kernel
+// template cannot instantiate this builtin and would silently drop the stub).
+__device__ __forceinline__ void buffer_load_lds16(__amdgpu_buffer_rsrc_t rsrc, unsigned lds_byte_addr, int voffset,
+                                                  int soffset) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, reinterpret_cast<__attribute__((address_space(3))) void*>(uintptr_t(lds_byte_addr)),
+                                           16, voffset, soffset, 0, 0);
+}
+__device__ __forceinline__ void buffer_load_lds4(__amdgpu_buffer_rsrc_t rsrc, unsigned lds_byte_addr, int voffset,
+                                                 int soffset) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, reinterpret_cast<__attribute__((address_space(3))) void*>(uintptr_t(lds_byte_addr)),
+                                           4, voffset, soffset, 0, 0);
+}
+
 // Diagnostic build only (MANO_PAIR_STAMP=1, tools/debug/pair_stamps.py): per
 // wave the shader-clock cycles from entry to exit, the cycles spent in the
 // hand-over polls and the units handled, read back by mano_debug_pair_stamps().
@@ -408,28 +439,33 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #endif
 #if MANO_PAIR_STAMP
 constexpr int kPairStampWaves = 256 * 12;
-__device__ unsigned long long g_pair_stamps[kPairStampWaves * 4];
+__device__ unsigned long long g_pair_stamps[kPairStampWaves * 8];
 struct PairStamp {
-  unsigned long long t0, wait = 0, units = 0;
+  unsigned long long t0, wait = 0, units = 0, t_stage = 0, t_store = 0, t_fetch = 0;
   __device__ PairStamp() : t0(__builtin_amdgcn_s_memtime()) {}
   __device__ void done(int wave) {
     const int w = blockIdx.x * 12 + wave;
     if ((threadIdx.x & 63) == 0 && w < kPairStampWaves) {
-      volatile unsigned long long* p = g_pair_stamps + w * 4;
+      volatile unsigned long long* p = g_pair_stamps + w * 8;
       p[0] = __builtin_amdgcn_s_memtime() - t0;
       p[1] = wait;
       p[2] = units;
       p[3] = 1;
+      p[4] = t_stage;
+      p[5] = t_store;
+      p[6] = t_fetch;
     }
   }
 };
 #define PAIR_TIMED(expr, st) ({ const unsigned long long _t = __builtin_amdgcn_s_memtime(); auto _r = (expr); st.wait += __builtin_amdgcn_s_memtime() - _t; _r; })
+#define PAIR_TIMED_STMT(stmt, field) do { const unsigned long long _t = __builtin_amdgcn_s_memtime(); stmt; stamp.field += __builtin_amdgcn_s_memtime() - _t; } while (0)
 #else
 struct PairStamp {
   unsigned long long units = 0;
   __device__ void done(int) {}
 };
 #define PAIR_TIMED(expr, st) (expr)
+#define PAIR_TIMED_STMT(stmt, field) stmt
 #endif
 
 template <bool kTrans>
@@ -474,9 +510,147 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
   int s = int(worker - qd * spans);
   if (qd >= n_quads) return;
 
+  static_assert(MANO_PAIR_DMA ? kPairSlots >= 2 * kPairCompute : kPairSlots == 2 * kPairCompute,
+                "slot count: the register-staging path keeps exactly two units in flight");
   PairStamp stamp;
   if (is_mem) {
     if (MANO_QUAD_PAIR_PRIO) __builtin_amdgcn_s_setprio(MANO_QUAD_PAIR_PRIO);
+#if MANO_PAIR_DMA
+    {
+      // The memory wave with LDS-DMA loads: unit k + 2's rows, transforms
+      // and translations go straight from HBM into its stage slot (buffer
+      // loads with the lds bit: lane i's 16 B land at M0 + 16 i), so a step
+      // has no register staging: wait until unit k's DMA has landed, signal,
+      // store unit k - 2 once skinned, then DMA unit k + 2 into the slot the
+      // store has just read out.  Each row is one DMA of its 48 (full span)
+      // or tail_rf4 (tail) float4, so the stage keeps its padded row stride.
+      // Rows and hands past the batch end fall outside num_records: their
+      // loads write zeros, their stores are dropped.
+      const int tail_rf4 = 3 * (n_verts - tail_v0) / 4;
+      int fvo[kQF4], tvo[kQF4];                 // store sweep: global byte offsets in the unit's rows
+      unsigned fso[kQF4], tso[kQF4];            // store sweep: LDS byte addresses in slot 0
+      const unsigned slot0 = lds_addr(reinterpret_cast<const int*>(&sh.slot[pair][0]));
+#pragma unroll
+      for (int i = 0; i < kQF4; ++i) {
+        const int idx = 64 * i + lane;
+        const int fr = idx / kQRowF4, fc = 4 * (idx % kQRowF4);
+        const int it = min(idx, kQHands * tail_rf4 - 1);
+        const int tr = it / tail_rf4, tc = 4 * (it % tail_rf4);
+        fvo[i] = 4 * (fr * vstride + fc);
+        tvo[i] = 4 * (tr * vstride + tc);
+        fso[i] = slot0 + unsigned(offsetof(QuadStage, rows)) + 4u * unsigned(fr * kQStride + fc);
+        tso[i] = slot0 + unsigned(offsetof(QuadStage, rows)) + 4u * unsigned(tr * kQStride + tc);
+      }
+      int rvo[kQHands];  // DMA: lane's byte offset in row r of the unit
+#pragma unroll
+      for (int r = 0; r < kQHands; ++r) rvo[r] = 4 * r * vstride + 16 * lane;
+      constexpr int kRsrcFlags = 0x00020000;  // gfx9 raw buffer
+      auto rsrc = [&](const float* base, int64_t floats) {
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, int(floats * 4), kRsrcFlags);
+      };
+      const unsigned slot0_s = __builtin_amdgcn_readfirstlane(slot0);
+      auto lds_at = [&](int slot, unsigned byte_off) {
+        return slot0_s + unsigned(slot) * unsigned(sizeof(QuadStage)) + byte_off;
+      };
+      // VMEM ops per DMA: 4 rows + 3 transform sweeps (+ 1 translations)
+      constexpr int kDmaOps = kQHands + kQTrF4 + (kTrans ? 1 : 0);
+      auto dma = [&](int64_t fq, int fs, int slot) {
+        const int64_t h0 = fq * kQHands;
+        const int valid = int(n - h0 < kQHands ? n - h0 : kQHands);
+        const auto rv = rsrc(vposed + h0 * vstride, int64_t(valid) * vstride);
+        const auto rt = rsrc(transforms + h0 * kTransformFloats, int64_t(valid) * kTransformFloats);
+        const bool full = fs < n_full;
+        const int soff = 4 * 3 * (full ? kQVerts * fs : tail_v0);
+        const int row_f4 = full ? kQRowF4 : tail_rf4;
+#pragma unroll
+        for (int i = 0; i < kQTrF4; ++i)
+          buffer_load_lds16(rt, lds_at(slot, unsigned(offsetof(QuadStage, tr)) + 1024u * i), 16 * lane,
+                                         1024 * i);
+        if constexpr (kTrans) {
+          const auto rr = rsrc(trans + h0 * 3, int64_t(valid) * 3);
+          if (lane < 12)
+            buffer_load_lds4(rr, lds_at(slot, unsigned(offsetof(QuadStage, trans))), 4 * lane, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < kQHands; ++r)
+          if (lane < row_f4)
+            buffer_load_lds16(rv, lds_at(slot, unsigned(offsetof(QuadStage, rows)) + 4u * r * kQStride),
+                                             rvo[r], soff);
+      };
+      auto ds_read4 = [](unsigned addr) {
+        return *reinterpret_cast<const __attribute__((address_space(3))) f32x4*>(uintptr_t(addr));
+      };
+      constexpr unsigned kSlotBytes = sizeof(QuadStage);
+      auto store = [&](int64_t fq, int fs, unsigned slot, bool real) {
+        const unsigned so = slot * kSlotBytes;
+        const int64_t h0 = fq * kQHands;
+        const int valid = real ? int(n - h0 < kQHands ? n - h0 : kQHands) : 0;  // 0: every store dropped
+        const auto ro = rsrc(verts + h0 * vstride, int64_t(valid) * vstride);
+        const bool full = fs < n_full;
+        const int soff = 4 * 3 * (full ? kQVerts * fs : tail_v0);
+        f32x4 sdata[kQF4];
+#pragma unroll
+        for (int i = 0; i < kQF4; ++i) sdata[i] = ds_read4((full ? fso[i] : tso[i]) + so);
+#pragma unroll
+        for (int i = 0; i < kQF4; ++i)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sdata[i]), ro, full ? fvo[i] : tvo[i], soff,
+                                                 kPairNtStores);
+      };
+      // Units k + 1 .. k + kAhead - 1 are in flight while unit k is skinned;
+      // unit k + kAhead goes into unit k - 2's slot once that is stored.
+      constexpr int kAhead = kPairSlots - kPairCompute;
+      int64_t pend_q[kPairCompute + 1];
+      int pend_s[kPairCompute + 1];
+      int k = 0;
+      bool ok = true;
+      int64_t qa = qd;  // unit k + kAhead (past the end: the current unit again)
+      int sa = s;
+      // Prologue: DMA units 0 .. kAhead - 1 with 3 (dropped) stores after
+      // each, so at every step's wait the ops issued after unit k's DMA are
+      // the same: kAhead - 1 times (3 stores + a DMA).
+      for (int j = 0; j < kAhead; ++j) {
+        if (j > 0) store(qd, s, 0, false);
+        dma(qa < n_quads ? qa : qd, qa < n_quads ? sa : s, j);
+        advance(qa, sa);
+      }
+      const int64_t n_units = (n_quads * spans - worker + n_workers - 1) / n_workers;  // >= 2
+      for (int64_t i = 0; i < n_units; ++i) {
+        // unit k = (qd, s) in slot k % kPairSlots: its DMA has landed once at
+        // most (kAhead - 1) (3 + kDmaOps) younger VMEM ops are outstanding.
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kAhead - 1) * (3 + kDmaOps)) : "memory");
+        pair_signal(full_flag, k + 1);
+#pragma unroll
+        for (int j = kPairCompute; j > 0; --j) pend_q[j] = pend_q[j - 1], pend_s[j] = pend_s[j - 1];
+        pend_q[0] = qd;
+        pend_s[0] = s;
+        if (k >= kPairCompute) {
+          const int ku = k - kPairCompute;
+          if (ok) ok = PAIR_TIMED(pair_wait_ge<MANO_PAIR_SLEEP_MEM>(&sh.done[pair][ku % kPairSlots], ku + 1), stamp);
+          ++stamp.units;
+          store(pend_q[kPairCompute], pend_s[kPairCompute], unsigned(ku % kPairSlots), true);
+        } else {
+          store(qd, s, 0, false);
+        }
+        // the store's LDS reads have returned (its data is in registers), so
+        // unit k - 2's slot is free for unit k + kAhead
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        dma(qa < n_quads ? qa : qd, qa < n_quads ? sa : s, (k + kAhead) % kPairSlots);
+        advance(qa, sa);
+        advance(qd, s);
+        ++k;
+      }
+      // the last min(k, 2) units
+      for (int i = min(k, kPairCompute) - 1; ok && i >= 0; --i) {
+        const int ku = k - 1 - i;
+        if (!pair_wait_ge<MANO_PAIR_SLEEP_MEM>(&sh.done[pair][ku % kPairSlots], ku + 1)) break;
+        store(pend_q[i], pend_s[i], unsigned(ku % kPairSlots), true);
+      }
+      // no LDS-DMA may still be writing when the workgroup's LDS is released
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      stamp.done(wave);
+      return;
+    }
+#endif
     // The memory wave shares its SIMD with the compute waves' f32 MFMAs,
     // which hold the VALU datapath: every VALU op here waits for one.  So
     // its per-unit work is buffer loads / stores and LDS accesses only --
@@ -598,8 +772,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     // Stage unit k from R, then (MANO_PAIR_STAGE_FIRST) store unit k - 2 once
     // skinned, then load unit k + 2 into R.
     auto stage_next = [&](MemRegs& R, bool store_prev) {
-      stage(s, unsigned(k % kPairSlots), R);
-      pair_signal(full_flag, k + 1);
+      PAIR_TIMED_STMT(stage(s, unsigned(k % kPairSlots), R); pair_signal(full_flag, k + 1), t_stage);
 #pragma unroll
       for (int i = kPairCompute; i > 0; --i) pend_q[i] = pend_q[i - 1], pend_s[i] = pend_s[i - 1];
       pend_q[0] = qd;
@@ -609,7 +782,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
         const int ku = k - kPairCompute;
         if (ok) ok = PAIR_TIMED(pair_wait_ge<MANO_PAIR_SLEEP_MEM>(&sh.done[pair][ku % kPairSlots], ku + 1), stamp);
         ++stamp.units;
-        store(pend_q[kPairCompute], pend_s[kPairCompute], unsigned(ku % kPairSlots));
+        PAIR_TIMED_STMT(store(pend_q[kPairCompute], pend_s[kPairCompute], unsigned(ku % kPairSlots)), t_store);
       } else {
         dummy_store();
       }
@@ -627,7 +800,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
         asm volatile("" ::"v"(d));
       }
 #endif
-      fetch(q2 < n_quads ? q2 : qd, q2 < n_quads ? s2 : s, R);
+      PAIR_TIMED_STMT(fetch(q2 < n_quads ? q2 : qd, q2 < n_quads ? s2 : s, R), t_fetch);
       keep_live();
       qd = q1;
       s = s1;
@@ -739,7 +912,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
 #if MANO_PAIR_STAMP
 }  // namespace mano
 extern "C" int mano_debug_pair_stamps(unsigned long long* host, int count) {
-  if (count > mano::kPairStampWaves * 4) count = mano::kPairStampWaves * 4;
+  if (count > mano::kPairStampWaves * 8) count = mano::kPairStampWaves * 8;
   return int(hipMemcpyFromSymbol(host, HIP_SYMBOL(mano::g_pair_stamps), size_t(count) * 8, 0,
                                  hipMemcpyDeviceToHost));
 }

@@ -27,7 +27,7 @@ for _ in range(300):
 torch.cuda.synchronize()
 lib = ctypes.CDLL(_abi.LIB_PATH)
 W = 256 * 12
-buf = (ctypes.c_ulonglong * (W * 4))()
+buf = (ctypes.c_ulonglong * (W * 8))()
 for rep in range(3):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -35,8 +35,8 @@ for rep in range(3):
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1)
-    assert lib.mano_debug_pair_stamps(buf, W * 4) == 0
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 12, 4).astype(np.int64)
+    assert lib.mano_debug_pair_stamps(buf, W * 8) == 0
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 12, 8).astype(np.int64)
     mem, cmp_ = a[:, :4], a[:, 4:]
     for name, r in (("memory", mem), ("compute", cmp_)):
         r = r[r[..., 3] == 1]
@@ -46,5 +46,9 @@ for rep in range(3):
               f"(p10 {np.percentile(wait / tot, 10) * 100:.1f}, p90 {np.percentile(wait / tot, 90) * 100:.1f}), "
               f"units median {np.median(units):.0f}, cycles/unit {np.median(tot / np.maximum(units, 1)):.0f}, "
               f"non-poll cycles/unit {np.median((tot - wait) / np.maximum(units, 1)):.0f}", flush=True)
+        if name == "memory":
+            u = np.maximum(units, 1)
+            print(f"      memory phases per unit: stage+signal {np.median(r[:, 4] / u):.0f}, "
+                  f"store {np.median(r[:, 5] / u):.0f}, fetch issue {np.median(r[:, 6] / u):.0f} cycles", flush=True)
     a[:] = 0
 m.close()
