@@ -639,11 +639,13 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
                   ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32));
   bs_stamp(5, (unsigned long long)(u_end - u));
   int n_ranges = 0;
+  unsigned long long t_first = 0, t_prologue = 0;  // cycles from a range's start to its first barrier
 #endif
 
   while (u < u_end) {
 #if MANO_BS_STAMP
     ++n_ranges;
+    const unsigned long long t_range = __builtin_amdgcn_s_memtime();
 #endif
     const int64_t quad = u / n_groups;
     const int g0 = int(u - quad * n_groups);
@@ -746,6 +748,13 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
     stage_w(g0, lds);
     stage_basis_tile16(basis16, 3 * g0 + 1, lds + kRingF4, wave, lane);
     bs_barrier<0>();  // the first two tiles and every prologue load have landed
+#if MANO_BS_STAMP
+    {
+      const unsigned long long dt = __builtin_amdgcn_s_memtime() - t_range;
+      if (n_ranges == 1) t_first = dt;
+      t_prologue += dt;
+    }
+#endif
 
     for (int grp = g0; grp < g1; ++grp) {
       const bool more = grp + 1 < g1;
@@ -818,6 +827,7 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
   bs_stamp(1, __builtin_amdgcn_s_memtime());
   bs_stamp(3, __builtin_amdgcn_s_memrealtime());
   bs_stamp(6, (unsigned long long)n_ranges);
+  bs_stamp(7, t_first | (t_prologue << 32));
 #endif
 }
 
@@ -1210,7 +1220,10 @@ namespace {
 // occupancy API only caps that, because it reads one block per CU high for
 // kernels using 97-112 SGPRs on gfx950 (MI355X_MICROARCH.md, correctness
 // boundaries).
-constexpr int kBlendSkinBlocksPerCU = 3;  // 168 VGPRs
+#ifndef MANO_BS_BLOCKS_PER_CU
+#define MANO_BS_BLOCKS_PER_CU 3  // diagnostic builds: fewer resident blocks per CU
+#endif
+constexpr int kBlendSkinBlocksPerCU = MANO_BS_BLOCKS_PER_CU;  // 168 VGPRs: 3 waves per SIMD
 constexpr int kSkinBlocksPerCU = MANO_SPAN_BLOCKS_PER_CU;  // skin_span
 
 template <class Kernel>

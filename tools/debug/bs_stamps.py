@@ -52,6 +52,11 @@ for rep in range(3):
     for rr in sorted(set(ranges.tolist())):
         s = ranges == rr
         print(f"  quads {rr}: {s.sum()} waves, end median {np.median(end[s]):.1f} max {end[s].max():.1f}")
+    t_first = (a[:, 7] & 0xFFFFFFFF) / clk  # us (cycles / MHz)
+    t_pro = (a[:, 7] >> 32) / clk
+    print(f"  first-range prologue (entry -> first barrier): median {np.median(t_first):.2f}  p90 "
+          f"{np.percentile(t_first, 90):.2f}  max {t_first.max():.2f} us; all range prologues per wave: median "
+          f"{np.median(t_pro):.2f} us ({np.median(t_pro / (end - start)) * 100:.1f} % of the wave's time)")
     ex = [np.median(end[xcc == x]) for x in range(8)]
     print("  end median per XCC:", " ".join(f"{e:.1f}" for e in ex))
     # per SIMD (xcc, se, cu, simd): the last exit of its waves
