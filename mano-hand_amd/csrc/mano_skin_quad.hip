@@ -57,8 +57,14 @@ typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
 #define MANO_QUAD_WAVES 8  // waves per block, one block per CU: 2 waves per SIMD
 #endif
 constexpr int kQWaves = MANO_QUAD_WAVES;
+#ifndef MANO_QUAD_P_EARLY
+#define MANO_QUAD_P_EARLY 1  // issue a unit's point reads before its transform-blend MFMAs
+#endif
+#ifndef MANO_QUAD_GROUP_MAJOR
+#define MANO_QUAD_GROUP_MAJOR 1  // transform-blend MFMAs and apply group by group (fewer live registers)
+#endif
 #ifndef MANO_QUAD_ABLATE
-#define MANO_QUAD_ABLATE 0  // diagnostic builds only: 1 = no LBS (skin_quad), 2 = no compute (skin_pair)
+#define MANO_QUAD_ABLATE 0  // diagnostic builds only: 1 = no LBS (skin_quad), 2 = no compute (skin_pair), 4 = no transform DMA (skin_pair)
 #endif
 constexpr int kQHands = 4;
 constexpr int kQVerts = 64;                                  // vertices per full span
@@ -104,6 +110,34 @@ __device__ __forceinline__ void skin_unit4_w(QuadStage& st, const f32x4 (&wf)[4]
     for (int t = 0; t < 3; ++t)
 #pragma unroll
       for (int c = 0; c < 3; ++c) p[g][t][c] = st.rows[hh[t] * kQStride + 3 * (lv[g] + v) + c];
+#if MANO_QUAD_P_EARLY
+  // The point reads issue before the MFMAs and land behind them (hipcc would
+  // sink them below the MFMAs to save registers, exposing their latency).
+  __builtin_amdgcn_sched_barrier(0);
+#endif
+#if MANO_QUAD_GROUP_MAJOR
+  // Group by group: its 3 chains of 4 MFMAs, then its apply -- 12 transform
+  // registers live instead of 48 (3 independent chains keep the f32 MFMA pipe
+  // full; the apply's VALU shares that datapath, so nothing overlaps anyway).
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    f32x4 T[3];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+        T[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][k], wf[g][k], k == 0 ? f32x4{} : T[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      float o = T[t][3];
+      o = fmaf(T[t][2], p[g][t][2], o);
+      o = fmaf(T[t][1], p[g][t][1], o);
+      o = fmaf(T[t][0], p[g][t][0], o);
+      if constexpr (kTrans) o = o + tr3[t];
+      st.rows[hh[t] * kQStride + 3 * (lv[g] + v) + cc[t]] = o;
+    }
+  }
+#else
   f32x4 T[NG][3];
 #pragma unroll
   for (int k = 0; k < 4; ++k)
@@ -123,6 +157,7 @@ __device__ __forceinline__ void skin_unit4_w(QuadStage& st, const f32x4 (&wf)[4]
       if constexpr (kTrans) o = o + tr3[t];
       st.rows[hh[t] * kQStride + 3 * (lv[g] + v) + cc[t]] = o;
     }
+#endif
 }
 
 // skin_unit4_w with the groups' W fragments read from the block's LDS copy.
@@ -553,7 +588,9 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
         return slot0_s + unsigned(slot) * unsigned(sizeof(QuadStage)) + byte_off;
       };
       // VMEM ops per DMA: 4 rows + 3 transform sweeps (+ 1 translations)
-      constexpr int kDmaOps = kQHands + kQTrF4 + (kTrans ? 1 : 0);
+      // (diagnostic MANO_QUAD_ABLATE & 4: no transform DMA -- stale operands, timing only)
+      constexpr int kTrOps = (MANO_QUAD_ABLATE & 4) ? 0 : kQTrF4;
+      constexpr int kDmaOps = kQHands + kTrOps + (kTrans ? 1 : 0);
       auto dma = [&](int64_t fq, int fs, int slot) {
         const int64_t h0 = fq * kQHands;
         const int valid = int(n - h0 < kQHands ? n - h0 : kQHands);
@@ -563,7 +600,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
         const int soff = 4 * 3 * (full ? kQVerts * fs : tail_v0);
         const int row_f4 = full ? kQRowF4 : tail_rf4;
 #pragma unroll
-        for (int i = 0; i < kQTrF4; ++i)
+        for (int i = 0; i < kTrOps; ++i)
           buffer_load_lds16(rt, lds_at(slot, unsigned(offsetof(QuadStage, tr)) + 1024u * i), 16 * lane,
                                          1024 * i);
         if constexpr (kTrans) {
@@ -617,7 +654,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       for (int64_t i = 0; i < n_units; ++i) {
         // unit k = (qd, s) in slot k % kPairSlots: its DMA has landed once at
         // most (kAhead - 1) (3 + kDmaOps) younger VMEM ops are outstanding.
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kAhead - 1) * (3 + kDmaOps)) : "memory");
+        PAIR_TIMED_STMT(asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kAhead - 1) * (3 + kDmaOps)) : "memory"), t_stage);
         pair_signal(full_flag, k + 1);
 #pragma unroll
         for (int j = kPairCompute; j > 0; --j) pend_q[j] = pend_q[j - 1], pend_s[j] = pend_s[j - 1];
@@ -627,14 +664,14 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
           const int ku = k - kPairCompute;
           if (ok) ok = PAIR_TIMED(pair_wait_ge<MANO_PAIR_SLEEP_MEM>(&sh.done[pair][ku % kPairSlots], ku + 1), stamp);
           ++stamp.units;
-          store(pend_q[kPairCompute], pend_s[kPairCompute], unsigned(ku % kPairSlots), true);
+          PAIR_TIMED_STMT(store(pend_q[kPairCompute], pend_s[kPairCompute], unsigned(ku % kPairSlots), true), t_store);
         } else {
           store(qd, s, 0, false);
         }
         // the store's LDS reads have returned (its data is in registers), so
         // unit k - 2's slot is free for unit k + kAhead
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        dma(qa < n_quads ? qa : qd, qa < n_quads ? sa : s, (k + kAhead) % kPairSlots);
+        PAIR_TIMED_STMT(dma(qa < n_quads ? qa : qd, qa < n_quads ? sa : s, (k + kAhead) % kPairSlots), t_fetch);
         advance(qa, sa);
         advance(qd, s);
         ++k;

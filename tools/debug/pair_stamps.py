@@ -48,7 +48,7 @@ for rep in range(3):
               f"non-poll cycles/unit {np.median((tot - wait) / np.maximum(units, 1)):.0f}", flush=True)
         if name == "memory":
             u = np.maximum(units, 1)
-            print(f"      memory phases per unit: stage+signal {np.median(r[:, 4] / u):.0f}, "
-                  f"store {np.median(r[:, 5] / u):.0f}, fetch issue {np.median(r[:, 6] / u):.0f} cycles", flush=True)
+            print(f"      memory phases per unit: stage / DMA wait {np.median(r[:, 4] / u):.0f}, "
+                  f"store {np.median(r[:, 5] / u):.0f}, fetch / DMA issue {np.median(r[:, 6] / u):.0f} cycles", flush=True)
     a[:] = 0
 m.close()
