@@ -393,17 +393,10 @@ __global__ __launch_bounds__(256, 2) void blend_kernel(
 // each other's barrier / LDS / store stalls.
 // ---------------------------------------------------------------------------
 typedef float f32x4v __attribute__((ext_vector_type(4)));
-#ifndef MANO_BS_SPLIT
-#define MANO_BS_SPLIT 0  // experiment: two interleaved accumulators per GEMM tile chain
-#endif
-
 __device__ __forceinline__ f32x4 mfma16_tile(const float (&a)[kGroups16 * 4],
                                              const f32x4* __restrict__ b, int lane) {
   f32x4 acc = {};
   f32x4 bn = b[lane];
-#if MANO_BS_SPLIT
-  f32x4 acc1 = {};
-#endif
 #pragma unroll
   for (int g = 0; g < kGroups16; ++g) {
     const f32x4 bv = bn;
@@ -411,18 +404,8 @@ __device__ __forceinline__ f32x4 mfma16_tile(const float (&a)[kGroups16 * 4],
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-#if MANO_BS_SPLIT
-      if (4 * g + q < kSteps16) {
-        if (q & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[4 * g + q], bv[q], acc1, 0, 0, 0);
-        else acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[4 * g + q], bv[q], acc, 0, 0, 0);
-      }
-#else
       if (4 * g + q < kSteps16) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[4 * g + q], bv[q], acc, 0, 0, 0);
-#endif
   }
-#if MANO_BS_SPLIT
-  acc += acc1;
-#endif
   return acc;
 }
 
@@ -577,9 +560,6 @@ __device__ __forceinline__ void store_out(float* dst, f32x3 v) {
   if constexpr (kNt) __builtin_nontemporal_store(v, reinterpret_cast<f32x3*>(dst));
   else *reinterpret_cast<f32x3*>(dst) = v;
 }
-#ifndef MANO_BS_SLOTS
-#define MANO_BS_SLOTS 3  // blend_skin16 basis ring: 3 slots (DMA 2 tiles ahead) or 4 (3 ahead)
-#endif
 
 // Fused blend GEMM + LBS.  A block owns a contiguous range of (quad of 4
 // hand tiles, vertex group) units; at each quad its waves load their A
@@ -617,7 +597,7 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
   // One slot: a basis tile (10 KB) + the group's W fragment (1 KB, with the
   // group's first tile); ring of 3.
   constexpr int kRingF4 = (kGroups16 + 1) * 64;
-  constexpr int kSlots = MANO_BS_SLOTS;
+  constexpr int kSlots = 3;
   constexpr int kStores = (MANO_BS_ABLATE & 1) ? 0 : kVposed ? 8 : 4;  // global_store_dwordx3 per group
   // vmcnt of the barrier after tile t: the wave's memory ops issued after tile
   // t + 1's DMA -- tile t + 2's DMA (at least 2 pieces per wave) and, after a
@@ -698,52 +678,6 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
                                          16, 0, 0);
       }
     };
-#if MANO_BS_SLOTS == 4
-    // Ring of 4 slots, tile t in slot t & 3, DMA three tiles ahead: a group's
-    // stores are followed by two tile DMAs before a barrier waits on a DMA
-    // issued after them (vmcnt retires in issue order), so the stores get two
-    // tile times to drain instead of one.
-    auto slot = [&](int t) { return lds + (t & 3) * kRingF4; };
-    stage_basis_tile16(basis16, 3 * g0, slot(3 * g0), wave, lane);
-    stage_w(g0, slot(3 * g0));
-    stage_basis_tile16(basis16, 3 * g0 + 1, slot(3 * g0 + 1), wave, lane);
-    stage_basis_tile16(basis16, 3 * g0 + 2, slot(3 * g0 + 2), wave, lane);
-    bs_barrier<0>();
-    for (int grp = g0; grp < g1; ++grp) {
-      const bool more = grp + 1 < g1;
-      const int t0 = 3 * grp;
-      f32x4 p[3];
-      // Barrier after tile t waits for tile t + 1's DMA.  Younger ops then:
-      // q = 0, 1 -- two tiles' DMA and the previous group's stores; q = 2 --
-      // two tiles' DMA.  Last group of the range (no DMA ahead): q = 0 --
-      // one tile's DMA + the stores, q = 1, 2 -- the stores.
-      const f32x4 wf = slot(t0)[kGroups16 * 64 + lane];
-      if (more) {
-        prio_up<kDmaPrio>();
-        if constexpr (!(MANO_BS_ABLATE & 16)) stage_basis_tile16(basis16, t0 + 3, slot(t0 + 3), wave, lane);
-        stage_w(grp + 1, slot(t0 + 3));
-        prio_down<kDmaPrio>();
-      }
-      p[0] = mfma16_tile(a, slot(t0), lane);
-      if (more) bs_barrier<2 * kPieces + kStores>();
-      else bs_barrier<kPieces + kStores>();
-      if (more) {
-        prio_up<kDmaPrio>();
-        if constexpr (!(MANO_BS_ABLATE & 16)) stage_basis_tile16(basis16, t0 + 4, slot(t0 + 4), wave, lane);
-        prio_down<kDmaPrio>();
-      }
-      p[1] = mfma16_tile(a, slot(t0 + 1), lane);
-      if (more) bs_barrier<2 * kPieces + kStores>();
-      else bs_barrier<kStores>();
-      if (more) {
-        prio_up<kDmaPrio>();
-        if constexpr (!(MANO_BS_ABLATE & 16)) stage_basis_tile16(basis16, t0 + 5, slot(t0 + 5), wave, lane);
-        prio_down<kDmaPrio>();
-      }
-      p[2] = mfma16_tile(a, slot(t0 + 2), lane);
-      if (more) bs_barrier<2 * kPieces>();
-      else bs_barrier<kStores>();
-#else
     stage_basis_tile16(basis16, 3 * g0, lds, wave, lane);
     stage_w(g0, lds);
     stage_basis_tile16(basis16, 3 * g0 + 1, lds + kRingF4, wave, lane);
@@ -784,7 +718,6 @@ __global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
       p[2] = mfma16_tile(a, lds + 2 * kRingF4, lane);
       if (more) bs_barrier<kPieces>();
       else bs_barrier<0>();
-#endif
       int vb = grp * 16;
       if (vb > n_verts - 16) vb = n_verts - 16;
       const int voff = 3 * (vb + col);
@@ -893,185 +826,6 @@ __global__ __launch_bounds__(256, MANO_SPAN_BLOCKS_PER_CU) void skin_span_kernel
                   int(threadIdx.x & 63));
 }
 
-#ifndef MANO_SKIN_RING
-#define MANO_SKIN_RING 0  // standalone LBS: skin_span (default) or skin_ring (split roles)
-#endif
-#if MANO_SKIN_RING
-// ---------------------------------------------------------------------------
-// skin_ring: the standalone LBS (mano_np.py:112-115) with split roles.  One
-// 8-wave block per CU: waves 0-3 compute, waves 4-7 load; pair w = (compute
-// wave w, load wave w + 4) shares a SIMD.  Full 64-vertex spans (units of 16
-// hands x 64 vertices, as skin_span) flow through three LDS slots per pair
-// in lock-step phases:
-//   phase p   load wave: LDS-DMA of unit(p) into slot p % 3, one 768-B row per
-//             global_load_lds_dwordx4 on 48 lanes (padded row stride, so the
-//             D-layout point reads are conflict-free); two units per pair stay
-//             in flight (the barrier waits only for unit(p - 1));
-//             compute wave: skins unit(p - 2) from slot (p - 2) % 3 with
-//             blend_skin16's MFMA transform tiles and fmaf order (bit-exact
-//             with the fused kernel) and stores the points straight from
-//             registers (12-B rows, as blend_skin16); its operands (transform
-//             fragments, weights, trans) are fetched one phase ahead;
-//   one workgroup barrier (load: unit(p - 1) landed -- counted vmcnt;
-//   compute: its slot reads done).
-// The compute wave never waits on HBM loads and the load wave never on the
-// MFMA pipe.  Units go to pairs in grid-stride order (XCD-aware pair ids), so
-// the chip streams a compact window.  The n_verts % 64 tail of each tile runs
-// after the ring on the compute waves through the per-group point path.
-// ---------------------------------------------------------------------------
-constexpr int kRingPairs = 4;
-constexpr int kRingSlots = 3;
-constexpr int kRingLdsBytes = kRingSlots * kRingPairs * span::kStageFloats * 4;  // 150,528 B
-constexpr int kRingRowLanes = 3 * span::kVerts / 4;  // 48 lanes x 16 B = one 768-B span row
-
-// One LDS-DMA row: lanes 0..47 each move 16 B (global_load_lds_dwordx4) from
-// their source into lds_dst + 16 x lane.  (global_load_lds_dwordx3 writes lane
-// l at lds_dst + 16 l as well, not 12 l -- tools/microbench/lds_dma_x3.hip --
-// and the x4 form reads 4-B-aligned sources correctly.)  The load wave reads
-// no LDS itself, so hipcc's view of the DMA as a pending LDS write costs
-// nothing; the phase barrier's counted vmcnt orders it for the readers.
-__device__ __forceinline__ void dma_row(const float* gsrc, float* lds_dst) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
-                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
-}
-
-template <bool kTrans>
-__global__ __launch_bounds__(512, 1) void skin_ring_kernel(
-    const float* __restrict__ transforms, const float* __restrict__ wfrag16,
-    const float* __restrict__ vposed, const float* __restrict__ trans, float* __restrict__ verts,
-    int64_t n, int n_verts, int n_groups) {
-  extern __shared__ float ring_lds[];
-  using Lbs = SpanLbs16<kTrans>;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int w = wave & (kRingPairs - 1);
-  const bool is_load = wave >= kRingPairs;
-  int lane = threadIdx.x & 63;
-  asm volatile("" : "+v"(lane));
-  const int vstride = 3 * n_verts;
-  const int n_full = n_verts / span::kVerts;
-  const int n_tail = n_groups - span::kGroups * n_full;
-  const int64_t nt16 = (n + 15) / 16;
-  const int64_t units = nt16 * n_full;
-  const int64_t b = blockIdx.x, nb = gridDim.x;
-  const int64_t blk = (nb % 8) ? b : (b % 8) * (nb / 8) + b / 8;  // XCD-aware (L2 locality only)
-  const int64_t pair = blk * kRingPairs + w;
-  const int64_t n_pairs = nb * kRingPairs;
-  const int64_t n_phases = (units + n_pairs - 1) / n_pairs;
-  const int row0 = 4 * (lane >> 4), col = lane & 15;
-  auto slot = [&](int64_t p) {
-    return ring_lds + (int(p % kRingSlots) * kRingPairs + w) * span::kStageFloats;
-  };
-  auto unit_ok = [&](int64_t p) { return p >= 0 && p < n_phases && p * n_pairs + pair < units; };
-  auto rows_of = [&](int64_t t) {
-    const int64_t left = n - 16 * t;
-    return int(left < 16 ? left : 16);
-  };
-
-  // The two roles run separate loops with the same barrier count, so the
-  // compiler's wait analysis of one never leaks into the other (a merged loop
-  // made the load wave wait vmcnt(0) on the compute wave's operand copies).
-  if (is_load) {
-    for (int64_t p = 0; p < n_phases + 2; ++p) {
-      if (unit_ok(p)) {
-        const int64_t u = p * n_pairs + pair;
-        const int64_t t = u / n_full;
-        const int sp = int(u - t * n_full);
-        const int n_valid = rows_of(t);
-        const float* src = vposed + 16 * t * int64_t(vstride) + 3 * span::kVerts * sp + 4 * lane;
-        float* dst = slot(p);
-        if (lane < kRingRowLanes) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int rr = r < n_valid ? r : n_valid - 1;  // rows past the batch end repeat the last hand
-            dma_row(src + unsigned(rr * vstride), dst + r * span::kStride);
-          }
-        }
-        // unit(p - 1) has landed; unit(p)'s 16 rows stay in flight
-        asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-      }
-    }
-    return;
-  }
-
-  // Compute waves: two operand sets in ping-pong (unit(q) is skinned at phase
-  // q + 2 with set a for even q, b for odd q, its operands loaded one phase
-  // earlier), so no register copy -- and no wait for this wave's in-flight
-  // stores -- sits between the phases.
-  Lbs lbs_a{transforms, wfrag16, trans, {}}, lbs_b{transforms, wfrag16, trans, {}};
-  f32x4 w_a[span::kGroups], w_b[span::kGroups];
-  auto prefetch = [&](int64_t p, Lbs& into, f32x4 (&w_into)[span::kGroups]) {  // operands of unit(p)
-    const int64_t u = p * n_pairs + pair;
-    const int64_t t = u / n_full;
-    const int sp = int(u - t * n_full);
-    into.fetch_tile(16 * t, n, rows_of(t), lane, into.cur);
-#pragma unroll
-    for (int g = 0; g < span::kGroups; ++g) w_into[g] = into.load_w(span::kGroups * sp + g, lane);
-  };
-  auto step = [&](int64_t p, Lbs& use, f32x4 (&w_use)[span::kGroups], Lbs& pf,
-                  f32x4 (&w_pf)[span::kGroups]) {
-    if (p >= n_phases + 2) return;
-    if (unit_ok(p - 2)) {  // unit(p - 1) is then the next one, if any
-      const int64_t u = (p - 2) * n_pairs + pair;
-      const int64_t t = u / n_full;
-      const int sp = int(u - t * n_full);
-      const int n_valid = rows_of(t);
-      if (unit_ok(p - 1)) prefetch(p - 1, pf, w_pf);
-      const float* st = slot(p - 2);
-      float* dst = verts + 16 * t * int64_t(vstride) + 3 * span::kVerts * sp;
-#pragma unroll
-      for (int g = 0; g < span::kGroups; ++g) {
-        float pts[4][3], o[4][3];
-        span::read_points(st, lane, g, pts);
-        use.apply(w_use[g], pts, o);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const unsigned off = unsigned(min(row0 + r, n_valid - 1) * vstride + 3 * (16 * g + col));
-          *reinterpret_cast<f32x3*>(dst + off) = f32x3{o[r][0], o[r][1], o[r][2]};
-        }
-        __builtin_amdgcn_sched_barrier(0);  // one group's LBS temporaries live at a time
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  };
-  if (unit_ok(0)) prefetch(0, lbs_a, w_a);
-  for (int64_t p = 0; p < n_phases + 2; p += 2) {
-    step(p, lbs_a, w_a, lbs_b, w_b);
-    step(p + 1, lbs_b, w_b, lbs_a, w_a);
-  }
-  Lbs& lbs = lbs_a;
-  if (n_tail == 0) return;
-
-  // The tail groups of every tile (vertices past the last full span), on the
-  // compute waves: points straight from HBM, the last group shifted to end at
-  // n_verts (skin_span's tail path).
-  for (int64_t t = pair; t < nt16; t += n_pairs) {
-    const int n_valid = rows_of(t);
-    lbs.fetch_tile(16 * t, n, n_valid, lane, lbs.cur);
-    const float* src = vposed + 16 * t * int64_t(vstride);
-    float* dst = verts + 16 * t * int64_t(vstride);
-    for (int g = 0; g < n_tail; ++g) {
-      const int vb = min(16 * (span::kGroups * n_full + g), n_verts - 16);
-      const f32x4 wg = lbs.load_w(span::kGroups * n_full + g, lane);
-      float pts[4][3], o[4][3];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const unsigned off = unsigned(min(row0 + r, n_valid - 1) * vstride + 3 * (vb + col));
-        const f32x3 v = *reinterpret_cast<const f32x3*>(src + off);
-#pragma unroll
-        for (int c = 0; c < 3; ++c) pts[r][c] = v[c];
-      }
-      lbs.apply(wg, pts, o);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const unsigned off = unsigned(min(row0 + r, n_valid - 1) * vstride + 3 * (vb + col));
-        *reinterpret_cast<f32x3*>(dst + off) = f32x3{o[r][0], o[r][1], o[r][2]};
-      }
-    }
-  }
-}
-#endif  // MANO_SKIN_RING
 
 // ---------------------------------------------------------------------------
 // PCA pose (mano_np.py:66-72) and standalone Rodrigues (:117-148).
@@ -1273,31 +1027,6 @@ hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* featu
 hipError_t launch_skin(const DeviceModel& m, int64_t n, const float* transforms,
                        const float* vposed, const float* trans, float* verts,
                        hipStream_t stream) {
-#if MANO_SKIN_RING
-  {
-    // 147 KB of dynamic LDS per block: raise the function's limit once.
-    static hipError_t attr = [] {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(skin_ring_kernel<true>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, kRingLdsBytes);
-      if (e == hipSuccess)
-        e = hipFuncSetAttribute(reinterpret_cast<const void*>(skin_ring_kernel<false>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kRingLdsBytes);
-      return e;
-    }();
-    if (attr != hipSuccess) return attr;
-    const int64_t nt16 = (n + 15) / 16;
-    const int64_t units = nt16 * (m.n_verts / span::kVerts);
-    int64_t blocks = std::max((units + kRingPairs - 1) / kRingPairs, (nt16 + kRingPairs - 1) / kRingPairs);
-    blocks = std::min<int64_t>(blocks, m.n_cu > 0 ? m.n_cu : 1);
-    auto launch = [&](auto kernel) {
-      hipLaunchKernelGGL(kernel, dim3(unsigned(blocks)), dim3(64 * 2 * kRingPairs), kRingLdsBytes, stream,
-                         transforms, m.wfrag16, vposed, trans, verts, n, m.n_verts, m.n_groups16);
-    };
-    if (trans) launch(skin_ring_kernel<true>);
-    else launch(skin_ring_kernel<false>);
-    return hipGetLastError();
-  }
-#endif
 #if MANO_SKIN_QUAD
   if (skin_quad_supported(m)) return launch_skin_quad(m, n, transforms, vposed, trans, verts, stream);
 #endif

@@ -389,12 +389,6 @@ __global__ __launch_bounds__(64 * kQWaves, 1) void skin_quad_kernel(
 #ifndef MANO_QUAD_PAIR_PRIO
 #define MANO_QUAD_PAIR_PRIO 0  // issue priority of the memory waves
 #endif
-#ifndef MANO_PAIR_NT
-#define MANO_PAIR_NT 0  // nontemporal memory-wave accesses: 1 = v_posed loads, 2 = verts stores, 4 = transforms loads
-#endif
-constexpr int kPairNtRows = (MANO_PAIR_NT & 1) ? 2 : 0;  // buffer cache-policy aux: 2 = nt on gfx950
-constexpr int kPairNtStores = (MANO_PAIR_NT & 2) ? 2 : 0;
-constexpr int kPairNtTr = (MANO_PAIR_NT & 4) ? 2 : 0;
 constexpr int kPairs = 4;
 constexpr int kPairCompute = MANO_QUAD_PAIR_COMPUTE;
 #ifndef MANO_PAIR_SLOTS
@@ -420,15 +414,6 @@ __device__ __forceinline__ unsigned lds_addr(const int* p) {
 }
 // Bounded: false after ~2^20 polls (tens of ms), and the caller then stops
 // -- a lost hand-over ends the kernel with wrong results, never hangs it.
-#ifndef MANO_PAIR_DMA
-#define MANO_PAIR_DMA 1  // memory wave loads with LDS-DMA (no register staging; 0: buffer loads into registers, then ds_write)
-#endif
-#ifndef MANO_PAIR_STAGE_FIRST
-#define MANO_PAIR_STAGE_FIRST 1  // memory step order: stage k, store k - 2, load k + 2 (0: store k - 2 first)
-#endif
-#ifndef MANO_PAIR_EXTRA_VALU
-#define MANO_PAIR_EXTRA_VALU 0
-#endif
 #ifndef MANO_PAIR_SLEEP_MEM
 #define MANO_PAIR_SLEEP_MEM 1  // s_sleep between the memory wave's polls (0 = none)
 #endif
@@ -545,158 +530,22 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
   int s = int(worker - qd * spans);
   if (qd >= n_quads) return;
 
-  static_assert(MANO_PAIR_DMA ? kPairSlots >= 2 * kPairCompute : kPairSlots == 2 * kPairCompute,
-                "slot count: the register-staging path keeps exactly two units in flight");
+  static_assert(kPairSlots >= 2 * kPairCompute, "slot count: the two units being skinned and one in flight");
   PairStamp stamp;
   if (is_mem) {
     if (MANO_QUAD_PAIR_PRIO) __builtin_amdgcn_s_setprio(MANO_QUAD_PAIR_PRIO);
-#if MANO_PAIR_DMA
-    {
-      // The memory wave with LDS-DMA loads: unit k + 2's rows, transforms
-      // and translations go straight from HBM into its stage slot (buffer
-      // loads with the lds bit: lane i's 16 B land at M0 + 16 i), so a step
-      // has no register staging: wait until unit k's DMA has landed, signal,
-      // store unit k - 2 once skinned, then DMA unit k + 2 into the slot the
-      // store has just read out.  Each row is one DMA of its 48 (full span)
-      // or tail_rf4 (tail) float4, so the stage keeps its padded row stride.
-      // Rows and hands past the batch end fall outside num_records: their
-      // loads write zeros, their stores are dropped.
-      const int tail_rf4 = 3 * (n_verts - tail_v0) / 4;
-      int fvo[kQF4], tvo[kQF4];                 // store sweep: global byte offsets in the unit's rows
-      unsigned fso[kQF4], tso[kQF4];            // store sweep: LDS byte addresses in slot 0
-      const unsigned slot0 = lds_addr(reinterpret_cast<const int*>(&sh.slot[pair][0]));
-#pragma unroll
-      for (int i = 0; i < kQF4; ++i) {
-        const int idx = 64 * i + lane;
-        const int fr = idx / kQRowF4, fc = 4 * (idx % kQRowF4);
-        const int it = min(idx, kQHands * tail_rf4 - 1);
-        const int tr = it / tail_rf4, tc = 4 * (it % tail_rf4);
-        fvo[i] = 4 * (fr * vstride + fc);
-        tvo[i] = 4 * (tr * vstride + tc);
-        fso[i] = slot0 + unsigned(offsetof(QuadStage, rows)) + 4u * unsigned(fr * kQStride + fc);
-        tso[i] = slot0 + unsigned(offsetof(QuadStage, rows)) + 4u * unsigned(tr * kQStride + tc);
-      }
-      int rvo[kQHands];  // DMA: lane's byte offset in row r of the unit
-#pragma unroll
-      for (int r = 0; r < kQHands; ++r) rvo[r] = 4 * r * vstride + 16 * lane;
-      constexpr int kRsrcFlags = 0x00020000;  // gfx9 raw buffer
-      auto rsrc = [&](const float* base, int64_t floats) {
-        return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, int(floats * 4), kRsrcFlags);
-      };
-      const unsigned slot0_s = __builtin_amdgcn_readfirstlane(slot0);
-      auto lds_at = [&](int slot, unsigned byte_off) {
-        return slot0_s + unsigned(slot) * unsigned(sizeof(QuadStage)) + byte_off;
-      };
-      // VMEM ops per DMA: 4 rows + 3 transform sweeps (+ 1 translations)
-      // (diagnostic MANO_QUAD_ABLATE & 4: no transform DMA -- stale operands, timing only)
-      constexpr int kTrOps = (MANO_QUAD_ABLATE & 4) ? 0 : kQTrF4;
-      constexpr int kDmaOps = kQHands + kTrOps + (kTrans ? 1 : 0);
-      auto dma = [&](int64_t fq, int fs, int slot) {
-        const int64_t h0 = fq * kQHands;
-        const int valid = int(n - h0 < kQHands ? n - h0 : kQHands);
-        const auto rv = rsrc(vposed + h0 * vstride, int64_t(valid) * vstride);
-        const auto rt = rsrc(transforms + h0 * kTransformFloats, int64_t(valid) * kTransformFloats);
-        const bool full = fs < n_full;
-        const int soff = 4 * 3 * (full ? kQVerts * fs : tail_v0);
-        const int row_f4 = full ? kQRowF4 : tail_rf4;
-#pragma unroll
-        for (int i = 0; i < kTrOps; ++i)
-          buffer_load_lds16(rt, lds_at(slot, unsigned(offsetof(QuadStage, tr)) + 1024u * i), 16 * lane,
-                                         1024 * i);
-        if constexpr (kTrans) {
-          const auto rr = rsrc(trans + h0 * 3, int64_t(valid) * 3);
-          if (lane < 12)
-            buffer_load_lds4(rr, lds_at(slot, unsigned(offsetof(QuadStage, trans))), 4 * lane, 0);
-        }
-#pragma unroll
-        for (int r = 0; r < kQHands; ++r)
-          if (lane < row_f4)
-            buffer_load_lds16(rv, lds_at(slot, unsigned(offsetof(QuadStage, rows)) + 4u * r * kQStride),
-                                             rvo[r], soff);
-      };
-      auto ds_read4 = [](unsigned addr) {
-        return *reinterpret_cast<const __attribute__((address_space(3))) f32x4*>(uintptr_t(addr));
-      };
-      constexpr unsigned kSlotBytes = sizeof(QuadStage);
-      auto store = [&](int64_t fq, int fs, unsigned slot, bool real) {
-        const unsigned so = slot * kSlotBytes;
-        const int64_t h0 = fq * kQHands;
-        const int valid = real ? int(n - h0 < kQHands ? n - h0 : kQHands) : 0;  // 0: every store dropped
-        const auto ro = rsrc(verts + h0 * vstride, int64_t(valid) * vstride);
-        const bool full = fs < n_full;
-        const int soff = 4 * 3 * (full ? kQVerts * fs : tail_v0);
-        f32x4 sdata[kQF4];
-#pragma unroll
-        for (int i = 0; i < kQF4; ++i) sdata[i] = ds_read4((full ? fso[i] : tso[i]) + so);
-#pragma unroll
-        for (int i = 0; i < kQF4; ++i)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sdata[i]), ro, full ? fvo[i] : tvo[i], soff,
-                                                 kPairNtStores);
-      };
-      // Units k + 1 .. k + kAhead - 1 are in flight while unit k is skinned;
-      // unit k + kAhead goes into unit k - 2's slot once that is stored.
-      constexpr int kAhead = kPairSlots - kPairCompute;
-      int64_t pend_q[kPairCompute + 1];
-      int pend_s[kPairCompute + 1];
-      int k = 0;
-      bool ok = true;
-      int64_t qa = qd;  // unit k + kAhead (past the end: the current unit again)
-      int sa = s;
-      // Prologue: DMA units 0 .. kAhead - 1 with 3 (dropped) stores after
-      // each, so at every step's wait the ops issued after unit k's DMA are
-      // the same: kAhead - 1 times (3 stores + a DMA).
-      for (int j = 0; j < kAhead; ++j) {
-        if (j > 0) store(qd, s, 0, false);
-        dma(qa < n_quads ? qa : qd, qa < n_quads ? sa : s, j);
-        advance(qa, sa);
-      }
-      const int64_t n_units = (n_quads * spans - worker + n_workers - 1) / n_workers;  // >= 2
-      for (int64_t i = 0; i < n_units; ++i) {
-        // unit k = (qd, s) in slot k % kPairSlots: its DMA has landed once at
-        // most (kAhead - 1) (3 + kDmaOps) younger VMEM ops are outstanding.
-        PAIR_TIMED_STMT(asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kAhead - 1) * (3 + kDmaOps)) : "memory"), t_stage);
-        pair_signal(full_flag, k + 1);
-#pragma unroll
-        for (int j = kPairCompute; j > 0; --j) pend_q[j] = pend_q[j - 1], pend_s[j] = pend_s[j - 1];
-        pend_q[0] = qd;
-        pend_s[0] = s;
-        if (k >= kPairCompute) {
-          const int ku = k - kPairCompute;
-          if (ok) ok = PAIR_TIMED(pair_wait_ge<MANO_PAIR_SLEEP_MEM>(&sh.done[pair][ku % kPairSlots], ku + 1), stamp);
-          ++stamp.units;
-          PAIR_TIMED_STMT(store(pend_q[kPairCompute], pend_s[kPairCompute], unsigned(ku % kPairSlots), true), t_store);
-        } else {
-          store(qd, s, 0, false);
-        }
-        // the store's LDS reads have returned (its data is in registers), so
-        // unit k - 2's slot is free for unit k + kAhead
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        PAIR_TIMED_STMT(dma(qa < n_quads ? qa : qd, qa < n_quads ? sa : s, (k + kAhead) % kPairSlots), t_fetch);
-        advance(qa, sa);
-        advance(qd, s);
-        ++k;
-      }
-      // the last min(k, 2) units
-      for (int i = min(k, kPairCompute) - 1; ok && i >= 0; --i) {
-        const int ku = k - 1 - i;
-        if (!pair_wait_ge<MANO_PAIR_SLEEP_MEM>(&sh.done[pair][ku % kPairSlots], ku + 1)) break;
-        store(pend_q[i], pend_s[i], unsigned(ku % kPairSlots), true);
-      }
-      // no LDS-DMA may still be writing when the workgroup's LDS is released
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      stamp.done(wave);
-      return;
-    }
-#endif
-    // The memory wave shares its SIMD with the compute waves' f32 MFMAs,
-    // which hold the VALU datapath: every VALU op here waits for one.  So
-    // its per-unit work is buffer loads / stores and LDS accesses only --
-    // all lane offsets are kernel constants, the unit moves the SGPR buffer
-    // bases, and rows past the batch end fall outside num_records (loads
-    // read 0, stores are dropped) instead of being clamped.
+    // The memory wave with LDS-DMA loads: unit k + 2's rows, transforms
+    // and translations go straight from HBM into its stage slot (buffer
+    // loads with the lds bit: lane i's 16 B land at M0 + 16 i), so a step
+    // has no register staging: wait until unit k's DMA has landed, signal,
+    // store unit k - 2 once skinned, then DMA unit k + 2 into the slot the
+    // store has just read out.  Each row is one DMA of its 48 (full span)
+    // or tail_rf4 (tail) float4, so the stage keeps its padded row stride.
+    // Rows and hands past the batch end fall outside num_records: their
+    // loads write zeros, their stores are dropped.
     const int tail_rf4 = 3 * (n_verts - tail_v0) / 4;
-    int fvo[kQF4], tvo[kQF4];                 // global byte offsets in the unit's rows
-    unsigned fso[kQF4], tso[kQF4], tro[kQTrF4];  // LDS byte addresses in slot 0
+    int fvo[kQF4], tvo[kQF4];                 // store sweep: global byte offsets in the unit's rows
+    unsigned fso[kQF4], tso[kQF4];            // store sweep: LDS byte addresses in slot 0
     const unsigned slot0 = lds_addr(reinterpret_cast<const int*>(&sh.slot[pair][0]));
 #pragma unroll
     for (int i = 0; i < kQF4; ++i) {
@@ -709,181 +558,114 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       fso[i] = slot0 + unsigned(offsetof(QuadStage, rows)) + 4u * unsigned(fr * kQStride + fc);
       tso[i] = slot0 + unsigned(offsetof(QuadStage, rows)) + 4u * unsigned(tr * kQStride + tc);
     }
+    int rvo[kQHands];  // DMA: lane's byte offset in row r of the unit
 #pragma unroll
-    for (int i = 0; i < kQTrF4; ++i) tro[i] = slot0 + unsigned(offsetof(QuadStage, tr)) + 16u * unsigned(64 * i + lane);
-    const unsigned trs = slot0 + unsigned(offsetof(QuadStage, trans)) + 4u * unsigned(min(lane, 15));
+    for (int r = 0; r < kQHands; ++r) rvo[r] = 4 * r * vstride + 16 * lane;
     constexpr int kRsrcFlags = 0x00020000;  // gfx9 raw buffer
     auto rsrc = [&](const float* base, int64_t floats) {
       return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, int(floats * 4), kRsrcFlags);
     };
-    // Two register sets: the loads of unit k + 2 go out while unit k + 1's
-    // are in flight (set k & 1; the loop below is unrolled by 2 so the set is
-    // a compile-time choice -- a runtime-indexed pair would go to scratch).
-    struct MemRegs {
-      f32x4 rb[kQF4], tb[kQTrF4];
-      float trb;
+    const unsigned slot0_s = __builtin_amdgcn_readfirstlane(slot0);
+    auto lds_at = [&](int slot, unsigned byte_off) {
+      return slot0_s + unsigned(slot) * unsigned(sizeof(QuadStage)) + byte_off;
     };
-    auto fetch = [&](int64_t fq, int fs, MemRegs& R) {
+    // VMEM ops per DMA: 4 rows + 3 transform sweeps (+ 1 translations)
+    // (diagnostic MANO_QUAD_ABLATE & 4: no transform DMA -- stale operands, timing only)
+    constexpr int kTrOps = (MANO_QUAD_ABLATE & 4) ? 0 : kQTrF4;
+    constexpr int kDmaOps = kQHands + kTrOps + (kTrans ? 1 : 0);
+    auto dma = [&](int64_t fq, int fs, int slot) {
       const int64_t h0 = fq * kQHands;
       const int valid = int(n - h0 < kQHands ? n - h0 : kQHands);
       const auto rv = rsrc(vposed + h0 * vstride, int64_t(valid) * vstride);
       const auto rt = rsrc(transforms + h0 * kTransformFloats, int64_t(valid) * kTransformFloats);
-#pragma unroll
-      for (int i = 0; i < kQTrF4; ++i)
-        R.tb[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * (64 * i + lane), 0, kPairNtTr));
-      if constexpr (kTrans) {
-        const auto rr = rsrc(trans + h0 * 3, int64_t(valid) * 3);
-        R.trb = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, 4 * lane, 0, 0));
-      }
       const bool full = fs < n_full;
       const int soff = 4 * 3 * (full ? kQVerts * fs : tail_v0);
+      const int row_f4 = full ? kQRowF4 : tail_rf4;
 #pragma unroll
-      for (int i = 0; i < kQF4; ++i)
-        R.rb[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, full ? fvo[i] : tvo[i], soff, kPairNtRows));
-    };
-    auto ds_write4 = [](unsigned addr, const f32x4& v) {
-      *reinterpret_cast<__attribute__((address_space(3))) f32x4*>(uintptr_t(addr)) = v;
+      for (int i = 0; i < kTrOps; ++i)
+        buffer_load_lds16(rt, lds_at(slot, unsigned(offsetof(QuadStage, tr)) + 1024u * i), 16 * lane,
+                                       1024 * i);
+      if constexpr (kTrans) {
+        const auto rr = rsrc(trans + h0 * 3, int64_t(valid) * 3);
+        if (lane < 12)
+          buffer_load_lds4(rr, lds_at(slot, unsigned(offsetof(QuadStage, trans))), 4 * lane, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < kQHands; ++r)
+        if (lane < row_f4)
+          buffer_load_lds16(rv, lds_at(slot, unsigned(offsetof(QuadStage, rows)) + 4u * r * kQStride),
+                                           rvo[r], soff);
     };
     auto ds_read4 = [](unsigned addr) {
       return *reinterpret_cast<const __attribute__((address_space(3))) f32x4*>(uintptr_t(addr));
     };
     constexpr unsigned kSlotBytes = sizeof(QuadStage);
-    auto stage = [&](int fs, unsigned slot, const MemRegs& R) {
-      const unsigned so = slot * kSlotBytes;
-#pragma unroll
-      for (int i = 0; i < kQTrF4; ++i) ds_write4(tro[i] + so, R.tb[i]);
-      if constexpr (kTrans) {
-        if (lane < 12) *reinterpret_cast<__attribute__((address_space(3))) float*>(uintptr_t(trs + so)) = R.trb;
-      }
-      if (fs < n_full) {
-#pragma unroll
-        for (int i = 0; i < kQF4; ++i) ds_write4(fso[i] + so, R.rb[i]);
-      } else {
-#pragma unroll
-        for (int i = 0; i < kQF4; ++i) ds_write4(tso[i] + so, R.rb[i]);
-      }
-    };
-    // The stored data stays live past the next unit's loads (keep_live), so
-    // those loads never reuse a register a store reads -- hipcc would first
-    // wait for that store.
-    f32x4 sdata[kQF4] = {};
-    auto keep_live = [&] {
-#pragma unroll
-      for (int i = 0; i < kQF4; ++i) asm volatile("" ::"v"(sdata[i]));
-    };
-    auto store = [&](int64_t fq, int fs, unsigned slot) {
+    auto store = [&](int64_t fq, int fs, unsigned slot, bool real) {
       const unsigned so = slot * kSlotBytes;
       const int64_t h0 = fq * kQHands;
-      const int valid = int(n - h0 < kQHands ? n - h0 : kQHands);
+      const int valid = real ? int(n - h0 < kQHands ? n - h0 : kQHands) : 0;  // 0: every store dropped
       const auto ro = rsrc(verts + h0 * vstride, int64_t(valid) * vstride);
       const bool full = fs < n_full;
       const int soff = 4 * 3 * (full ? kQVerts * fs : tail_v0);
+      f32x4 sdata[kQF4];
 #pragma unroll
       for (int i = 0; i < kQF4; ++i) sdata[i] = ds_read4((full ? fso[i] : tso[i]) + so);
 #pragma unroll
       for (int i = 0; i < kQF4; ++i)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sdata[i]), ro, full ? fvo[i] : tvo[i], soff, kPairNtStores);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sdata[i]), ro, full ? fvo[i] : tvo[i], soff,
+                                               0);
     };
-    // pend*: the units staged and not yet stored (0 = the latest);
-    // (q1, s1): the unit after the one to stage next, (q2, s2) the next but one.
+    // Units k + 1 .. k + kAhead - 1 are in flight while unit k is skinned;
+    // unit k + kAhead goes into unit k - 2's slot once that is stored.
+    constexpr int kAhead = kPairSlots - kPairCompute;
     int64_t pend_q[kPairCompute + 1];
     int pend_s[kPairCompute + 1];
     int k = 0;
     bool ok = true;
-    int64_t q1 = qd;
-    int s1 = s;
-    advance(q1, s1);
-    MemRegs RA, RB;
-    RA.trb = RB.trb = 0.f;
-#if MANO_PAIR_STAGE_FIRST
-    // A prologue step's stand-in for store(k - 2): the same 3 buffer stores
-    // through a resource of num_records 0 (every lane out of range: dropped),
-    // so prologue and steady steps issue the same memory operations.
-    auto dummy_store = [&] {
-      const auto ro = rsrc(verts, 0);
+    int64_t qa = qd;  // unit k + kAhead (past the end: the current unit again)
+    int sa = s;
+    // Prologue: DMA units 0 .. kAhead - 1 with 3 (dropped) stores after
+    // each, so at every step's wait the ops issued after unit k's DMA are
+    // the same: kAhead - 1 times (3 stores + a DMA).
+    for (int j = 0; j < kAhead; ++j) {
+      if (j > 0) store(qd, s, 0, false);
+      dma(qa < n_quads ? qa : qd, qa < n_quads ? sa : s, j);
+      advance(qa, sa);
+    }
+    const int64_t n_units = (n_quads * spans - worker + n_workers - 1) / n_workers;  // >= 2
+    for (int64_t i = 0; i < n_units; ++i) {
+      // unit k = (qd, s) in slot k % kPairSlots: its DMA has landed once at
+      // most (kAhead - 1) (3 + kDmaOps) younger VMEM ops are outstanding.
+      PAIR_TIMED_STMT(asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kAhead - 1) * (3 + kDmaOps)) : "memory"), t_stage);
+      pair_signal(full_flag, k + 1);
 #pragma unroll
-      for (int i = 0; i < kQF4; ++i)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sdata[i]), ro, fvo[i], 0, kPairNtStores);
-    };
-#endif
-    // Stage unit k from R, then (MANO_PAIR_STAGE_FIRST) store unit k - 2 once
-    // skinned, then load unit k + 2 into R.
-    auto stage_next = [&](MemRegs& R, bool store_prev) {
-      PAIR_TIMED_STMT(stage(s, unsigned(k % kPairSlots), R); pair_signal(full_flag, k + 1), t_stage);
-#pragma unroll
-      for (int i = kPairCompute; i > 0; --i) pend_q[i] = pend_q[i - 1], pend_s[i] = pend_s[i - 1];
+      for (int j = kPairCompute; j > 0; --j) pend_q[j] = pend_q[j - 1], pend_s[j] = pend_s[j - 1];
       pend_q[0] = qd;
       pend_s[0] = s;
-#if MANO_PAIR_STAGE_FIRST
-      if (store_prev) {
+      if (k >= kPairCompute) {
         const int ku = k - kPairCompute;
         if (ok) ok = PAIR_TIMED(pair_wait_ge<MANO_PAIR_SLEEP_MEM>(&sh.done[pair][ku % kPairSlots], ku + 1), stamp);
         ++stamp.units;
-        PAIR_TIMED_STMT(store(pend_q[kPairCompute], pend_s[kPairCompute], unsigned(ku % kPairSlots)), t_store);
+        PAIR_TIMED_STMT(store(pend_q[kPairCompute], pend_s[kPairCompute], unsigned(ku % kPairSlots), true), t_store);
       } else {
-        dummy_store();
+        store(qd, s, 0, false);
       }
-#else
-      (void)store_prev;
-#endif
-      int64_t q2 = q1;
-      int s2 = s1;
-      advance(q2, s2);
-#if MANO_PAIR_EXTRA_VALU  // diagnostic: N dependent VALU ops per unit in the memory wave
-      {
-        int d = lane;
-#pragma unroll
-        for (int e = 0; e < MANO_PAIR_EXTRA_VALU; ++e) asm volatile("v_add_u32 %0, 1, %0" : "+v"(d));
-        asm volatile("" ::"v"(d));
-      }
-#endif
-      PAIR_TIMED_STMT(fetch(q2 < n_quads ? q2 : qd, q2 < n_quads ? s2 : s, R), t_fetch);
-      keep_live();
-      qd = q1;
-      s = s1;
-      q1 = q2;
-      s1 = s2;
+      // the store's LDS reads have returned (its data is in registers), so
+      // unit k - 2's slot is free for unit k + kAhead
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      PAIR_TIMED_STMT(dma(qa < n_quads ? qa : qd, qa < n_quads ? sa : s, (k + kAhead) % kPairSlots), t_fetch);
+      advance(qa, sa);
+      advance(qd, s);
       ++k;
-    };
-    fetch(qd, s, RA);
-    fetch(q1 < n_quads ? q1 : qd, q1 < n_quads ? s1 : s, RB);
-    // The first kPairCompute (= 2) units are staged without a store; then
-    // each step stores unit k - kPairCompute (once skinned) BEFORE staging
-    // unit k, so every path into a stage's wait has the same memory ops
-    // after its loads (hipcc merges the paths' wait counts).
-    // (every pair has at least 2 units: launch_skin_quad sizes the grid so)
-    static_assert(kPairCompute == 2, "the prologue stages one unit per register set");
-    stage_next(RA, false);
-    stage_next(RB, false);
-    // Steady state: a fixed count of steps, unrolled by 2 with no exit in
-    // between, so every path into a step's stage has issued the same memory
-    // operations since that set's loads (the other set's loads and two
-    // stores): hipcc's merged wait then leaves the other set in flight.  A
-    // timed-out hand-over only marks the wave broken (later polls are
-    // skipped); the results are then wrong, the kernel still ends.
-    const int64_t n_units = (n_quads * spans - worker + n_workers - 1) / n_workers;  // >= 2
-    auto step = [&](MemRegs& R) {
-#if MANO_PAIR_STAGE_FIRST
-      stage_next(R, true);
-#else
-      const int ku = k - kPairCompute;
-      if (ok) ok = PAIR_TIMED(pair_wait_ge<MANO_PAIR_SLEEP_MEM>(&sh.done[pair][ku % kPairSlots], ku + 1), stamp);
-      ++stamp.units;
-      store(pend_q[kPairCompute - 1], pend_s[kPairCompute - 1], unsigned(ku % kPairSlots));
-      stage_next(R, false);
-#endif
-    };
-    for (int64_t i = 2; i + 1 < n_units; i += 2) {
-      step(RA);
-      step(RB);
     }
-    if (n_units % 2 == 1) step(RA);
-    // the last min(k, kPairCompute) units
+    // the last min(k, 2) units
     for (int i = min(k, kPairCompute) - 1; ok && i >= 0; --i) {
       const int ku = k - 1 - i;
       if (!pair_wait_ge<MANO_PAIR_SLEEP_MEM>(&sh.done[pair][ku % kPairSlots], ku + 1)) break;
-      store(pend_q[i], pend_s[i], unsigned(ku % kPairSlots));
+      store(pend_q[i], pend_s[i], unsigned(ku % kPairSlots), true);
     }
+    // no LDS-DMA may still be writing when the workgroup's LDS is released
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stamp.done(wave);
     return;
   }
