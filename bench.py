@@ -390,7 +390,7 @@ def main(argv=None):
                             "flop_per_hand": BLEND_FLOP_PER_HAND}
     if "skin" in ms:
         a = gbs(SKIN_BYTES_PER_HAND, ms["skin"])
-        kernels["skin"] = {"kernel": "skin_pair_kernel" if args.precision == "fp32" else "skin_span_h3_kernel",
+        kernels["skin"] = {"kernel": "skin_pair_kernel" if args.precision == "fp32" else "skin_pair_kernel (f16x3)",
                            "ms": ms["skin"], "bound": "hbm",
                            "achieved_GBs": a, "frac": a / PEAK_HBM_GBS,
                            "bytes_per_hand": SKIN_BYTES_PER_HAND}
@@ -414,7 +414,7 @@ def main(argv=None):
     if "skin" in ms_other:
         t = ms_other["skin"]
         kernels[f"skin_{other}"] = {
-            "kernel": "skin_span_h3_kernel" if other == "f16x3" else "skin_pair_kernel",
+            "kernel": "skin_pair_kernel (f16x3)" if other == "f16x3" else "skin_pair_kernel",
             "ms": t, "precision": other, "in_timed_path": False, "bound": "hbm",
             "achieved_GBs": gbs(SKIN_BYTES_PER_HAND, t),
             "frac": gbs(SKIN_BYTES_PER_HAND, t) / PEAK_HBM_GBS, "bytes_per_hand": SKIN_BYTES_PER_HAND}

@@ -84,7 +84,7 @@ hipError_t launch_skin(const DeviceModel& m, int64_t n, const float* transforms,
 bool skin_quad_supported(const DeviceModel& m);
 hipError_t launch_skin_quad(const DeviceModel& m, int64_t n, const float* transforms,
                             const float* vposed, const float* trans, float* verts,
-                            hipStream_t stream);
+                            hipStream_t stream, bool h3 = false);
 // f16x3 mode (mano_kernels_h3.hip): same operands and outputs as
 // launch_blend_skin / launch_skin.
 hipError_t launch_blend_skin_h3(const DeviceModel& m, int64_t n, const float* features,

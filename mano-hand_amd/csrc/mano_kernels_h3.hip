@@ -195,6 +195,9 @@ __device__ __forceinline__ void lbs_h3(const f16x8 (&F)[12], const f16x8& w1, co
     }
 }
 
+#ifndef MANO_H3_SKIN_PAIR
+#define MANO_H3_SKIN_PAIR 1  // standalone f16x3 LBS: skin_pair's structure (skin_span_h3 for what it does not take)
+#endif
 #ifndef MANO_H3_DMA_PRIO
 #define MANO_H3_DMA_PRIO 0  // blend_skin_h3: wave priority while issuing the next group's LDS-DMA (1 and 3 measured: within noise)
 #endif
@@ -504,6 +507,13 @@ hipError_t launch_blend_skin_h3(const DeviceModel& m, int64_t n, const float* fe
 hipError_t launch_skin_h3(const DeviceModel& m, int64_t n, const float* transforms,
                           const float* vposed, const float* trans, float* verts,
                           hipStream_t stream) {
+#if MANO_H3_SKIN_PAIR
+  // skin_pair's memory / compute waves with the f16x3 LBS (mano_skin_quad.hip)
+  if (skin_quad_supported(m)) {
+    const hipError_t e = launch_skin_quad(m, n, transforms, vposed, trans, verts, stream, true);
+    if (e != hipErrorNotSupported) return e;  // not supported: a batch below one block
+  }
+#endif
   const int64_t units = (n + 15) / 16 * span::n_spans(m.n_verts);
   auto launch = [&](auto kernel) {
     hipLaunchKernelGGL(kernel, persistent_grid_h3(kernel, m, units, 4, kSkinH3BlocksPerCU), dim3(256),

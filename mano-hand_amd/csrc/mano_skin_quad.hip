@@ -171,6 +171,50 @@ __device__ __forceinline__ void skin_unit4(QuadStage& st, const f32x4* w_lds, co
   skin_unit4_w<kTrans, NG>(st, wf, a, tr3, lv, hh, cc, v);
 }
 
+// The f16x3 precision mode (mano_kernels_h3.hip) on the same units: the
+// transform blend T[(hand, c, k)][v] = sum_j A_j[c][k] W[v][j] as two
+// v_mfma_f32_16x16x32_f16 per tile with every operand split into halves --
+// A = [Ah | Al] (x 2^kH3FrameExp, hi in lanes 0-31, lo in 32-63), W pieces
+// w1 = [Wh ; Wh], w2 = [Wl ; 0] (x 2^kH3WeightExp): T = A.w2 then += A.w1,
+// blend_skin_h3's products in its order -- then its apply:
+// out = fma(T3 + T2 z + T1 y + T0 x, 2^-(kH3FrameExp + kH3WeightExp), trans).
+// wl: per group 64 x 16 B, entries 0-31 = w1's lanes 0-31 (lanes 32-63 are
+// the same), 32-63 = w2's lanes 0-31 (lanes 32-63 are zero).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+template <bool kTrans, int NG = 4>
+__device__ __forceinline__ void skin_unit4_h3(QuadStage& st, const f16x8* wl, const f16x8 (&a)[3],
+                                              const float (&tr3)[3], const int (&G)[4], const int (&lv)[4],
+                                              const int (&hh)[3], const int (&cc)[3], int v, int lane,
+                                              float t_unscale) {
+  float p[NG][3][3];
+#pragma unroll
+  for (int g = 0; g < NG; ++g)
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) p[g][t][c] = st.rows[hh[t] * kQStride + 3 * (lv[g] + v) + c];
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const f16x8 w1 = wl[G[g] * 64 + (lane & 31)];
+    const f16x8 w2l = wl[G[g] * 64 + 32 + (lane & 31)];
+    const f16x8 w2 = lane < 32 ? w2l : f16x8{};
+    f32x4 T[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) T[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[t], w2, f32x4{}, 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) T[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[t], w1, T[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      float o = T[t][3];
+      o = fmaf(T[t][2], p[g][t][2], o);
+      o = fmaf(T[t][1], p[g][t][1], o);
+      o = fmaf(T[t][0], p[g][t][0], o);
+      st.rows[hh[t] * kQStride + 3 * (lv[g] + v) + cc[t]] = fmaf(o, t_unscale, kTrans ? tr3[t] : 0.f);
+    }
+  }
+}
+
 template <bool kTrans>
 __global__ __launch_bounds__(64 * kQWaves, 1) void skin_quad_kernel(
     const float* __restrict__ transforms, const float* __restrict__ wfrag16,
@@ -488,15 +532,25 @@ struct PairStamp {
 #define PAIR_TIMED_STMT(stmt, field) stmt
 #endif
 
-template <bool kTrans>
+// kH3: the f16x3 mode (skin_unit4_h3, W halves from basis_h3's pieces 30 /
+// 31, t_unscale); otherwise fp32 (wfrag16).
+template <bool kTrans, bool kH3 = false>
 __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     const float* __restrict__ transforms, const float* __restrict__ wfrag16,
     const float* __restrict__ vposed, const float* __restrict__ trans, float* __restrict__ verts,
-    int64_t n, int n_verts, int n_groups) {
+    int64_t n, int n_verts, int n_groups, const uint16_t* __restrict__ basis_h3, float t_unscale) {
   __shared__ f32x4 w_lds[kPairMaxGroups * 64];
   __shared__ PairShared sh;
-  for (int i = threadIdx.x; i < n_groups * 64; i += 64 * kPairWaves)
-    w_lds[i] = reinterpret_cast<const f32x4*>(wfrag16)[i];
+  for (int i = threadIdx.x; i < n_groups * 64; i += 64 * kPairWaves) {
+    if constexpr (kH3) {
+      const int grp = i >> 6, e = i & 63;
+      w_lds[i] = reinterpret_cast<const f32x4*>(basis_h3 + int64_t(grp) * kH3GroupHalves +
+                                                (kH3WPiece + (e >> 5)) * kH3PieceHalves)[e & 31];
+    } else {
+      w_lds[i] = reinterpret_cast<const f32x4*>(wfrag16)[i];
+    }
+  }
+
   if (threadIdx.x < kPairs) sh.full[threadIdx.x] = 0;
   if (threadIdx.x < kPairs * kPairSlots) sh.done[threadIdx.x / kPairSlots][threadIdx.x % kPairSlots] = 0;
   __syncthreads();
@@ -672,13 +726,14 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
 
   // compute wave
   const int q = lane >> 4, v = lane & 15;
-  int hh[3], cc[3], a_off[3];
+  int hh[3], cc[3], a_off[3], h3_off[3];
 #pragma unroll
   for (int t = 0; t < 3; ++t) {
     const int m0 = 16 * t + 4 * q, m = 16 * t + v;
     hh[t] = m0 / 12;
     cc[t] = (m0 % 12) / 4;
     a_off[t] = (m / 12) * kTransformFloats + 12 * q + m % 12;
+    h3_off[t] = (m / 12) * kTransformFloats + 12 * 8 * (q & 1) + m % 12;  // f16x3: joints 8 (q & 1) + j
   }
   // compute wave c of the pair takes the pair's units k = c, c + kPairCompute, ...
   const int cw = (wave - kPairs) / kPairs;
@@ -693,31 +748,65 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       for (int i = 0; i < kPairCompute; ++i) advance(qd, s);
       continue;
     }
-    float a[3][4], tr3[3];
+    float tr3[3];
 #pragma unroll
-    for (int t = 0; t < 3; ++t) {
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) a[t][kk] = st.tr[a_off[t] + 4 * 12 * kk];
-      tr3[t] = kTrans ? st.trans[3 * hh[t] + cc[t]] : 0.f;
-    }
+    for (int t = 0; t < 3; ++t) tr3[t] = kTrans ? st.trans[3 * hh[t] + cc[t]] : 0.f;
     // The unit's 4 groups (a tail unit: its n_tail groups, the last repeated
     // -- duplicates rewrite identical bits).  Every point is read before any
     // output lands: the tail's last group is shifted onto its neighbour's
     // vertices when n_verts % 16 != 0, and the skinning is in place.  Full
     // units get compile-time group offsets (LDS immediates).
-    if (s < n_full) {
-      const int G[4] = {4 * s, 4 * s + 1, 4 * s + 2, 4 * s + 3};
-      const int lv[4] = {0, 16, 32, 48};
-      skin_unit4<kTrans>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
-    } else {
-      int G[4], lv[4];
+    if constexpr (kH3) {
+      // A operands: row m = 16 t + (lane & 15) is (hand m / 12, c, k), K
+      // element j of the lane is joint 8 ((lane >> 4) & 1) + j, the hi half
+      // in lanes 0-31 and the lo half in 32-63 (blend_skin_h3's split).
+      f16x8 ah[3];
+      const bool lo = lane >= 32;
+      constexpr float kScale = float(1 << kH3FrameExp);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        G[g] = 4 * n_full + min(g, n_tail - 1);
-        lv[g] = min(16 * G[g], n_verts - 16) - tail_v0;
+      for (int t = 0; t < 3; ++t) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = st.tr[h3_off[t] + 12 * j] * kScale;
+          const _Float16 h = static_cast<_Float16>(x);
+          ah[t][j] = lo ? static_cast<_Float16>(x - static_cast<float>(h)) : h;
+        }
       }
-      if (n_tail == 1) skin_unit4<kTrans, 1>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
-      else skin_unit4<kTrans>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
+      const f16x8* wl = reinterpret_cast<const f16x8*>(w_lds);
+      if (s < n_full) {
+        const int G[4] = {4 * s, 4 * s + 1, 4 * s + 2, 4 * s + 3};
+        const int lv[4] = {0, 16, 32, 48};
+        skin_unit4_h3<kTrans>(st, wl, ah, tr3, G, lv, hh, cc, v, lane, t_unscale);
+      } else {
+        int G[4], lv[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          G[g] = 4 * n_full + min(g, n_tail - 1);
+          lv[g] = min(16 * G[g], n_verts - 16) - tail_v0;
+        }
+        if (n_tail == 1) skin_unit4_h3<kTrans, 1>(st, wl, ah, tr3, G, lv, hh, cc, v, lane, t_unscale);
+        else skin_unit4_h3<kTrans>(st, wl, ah, tr3, G, lv, hh, cc, v, lane, t_unscale);
+      }
+    } else {
+      float a[3][4];
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) a[t][kk] = st.tr[a_off[t] + 4 * 12 * kk];
+      if (s < n_full) {
+        const int G[4] = {4 * s, 4 * s + 1, 4 * s + 2, 4 * s + 3};
+        const int lv[4] = {0, 16, 32, 48};
+        skin_unit4<kTrans>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
+      } else {
+        int G[4], lv[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          G[g] = 4 * n_full + min(g, n_tail - 1);
+          lv[g] = min(16 * G[g], n_verts - 16) - tail_v0;
+        }
+        if (n_tail == 1) skin_unit4<kTrans, 1>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
+        else skin_unit4<kTrans>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
+      }
     }
     pair_signal(&sh.done[pair][k % kPairSlots], k + 1);
 #pragma unroll
@@ -747,9 +836,12 @@ bool skin_quad_supported(const DeviceModel& m) {
   return m.n_verts >= 16 && m.n_groups16 <= kQMaxGroups && (3 * (m.n_verts - tail_v0)) % 4 == 0;
 }
 
+// skin_pair (fp32, or f16x3 with h3) for the meshes skin_quad_supported
+// takes; a batch too small for one skin_pair block runs skin_quad_kernel
+// (fp32) or returns hipErrorNotSupported (f16x3: the caller's skin_span_h3).
 hipError_t launch_skin_quad(const DeviceModel& m, int64_t n, const float* transforms,
                             const float* vposed, const float* trans, float* verts,
-                            hipStream_t stream) {
+                            hipStream_t stream, bool h3) {
   if (n <= 0) return hipSuccess;
   const int spans = m.n_verts / kQVerts + (m.n_verts % kQVerts ? 1 : 0);
   const int64_t units = (n + kQHands - 1) / kQHands * spans;
@@ -760,6 +852,7 @@ hipError_t launch_skin_quad(const DeviceModel& m, int64_t n, const float* transf
   // at least 2 units per memory wave (its prologue stages two); a batch too
   // small for one block of those runs skin_quad_kernel
   blocks = std::min<int64_t>(units / (2 * kPairs), cap);
+  if (blocks < 1 && h3) return hipErrorNotSupported;
   if (blocks < 1) {
     auto launch1 = [&](auto kernel) {
       hipLaunchKernelGGL(kernel, dim3(1), dim3(64 * kQWaves), 0, stream, transforms, m.wfrag16, vposed,
@@ -771,10 +864,16 @@ hipError_t launch_skin_quad(const DeviceModel& m, int64_t n, const float* transf
   }
   auto launch = [&](auto kernel) {
     hipLaunchKernelGGL(kernel, dim3(unsigned(blocks)), dim3(64 * kPairWaves), 0, stream, transforms,
-                       m.wfrag16, vposed, trans, verts, n, m.n_verts, m.n_groups16);
+                       m.wfrag16, vposed, trans, verts, n, m.n_verts, m.n_groups16, m.basis_h3,
+                       m.h3_lbs_unscale);
   };
-  if (trans) launch(skin_pair_kernel<true>);
-  else launch(skin_pair_kernel<false>);
+  if (h3) {
+    if (trans) launch(skin_pair_kernel<true, true>);
+    else launch(skin_pair_kernel<false, true>);
+  } else {
+    if (trans) launch(skin_pair_kernel<true>);
+    else launch(skin_pair_kernel<false>);
+  }
   return hipGetLastError();
 #else
   auto launch = [&](auto kernel) {

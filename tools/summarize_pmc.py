@@ -26,6 +26,8 @@ FETCH_FACTOR = {"blend_skin": 2.0, "blend": 2.0, "skin": 2.0, "articulate": 2.0,
 
 
 def short(name):
+    if "::skin_pair_kernel<" in name and ", true>" in name.split("(")[1 if name.startswith("void") else 0]:
+        return "skin_h3"  # skin_pair_kernel<kTrans, kH3 = true>: the f16x3 standalone LBS
     for k, v in KERNELS.items():
         if "::" + k in name:
             return v

@@ -20,6 +20,8 @@ KERNELS = {"blend_skin16_kernel<": "blend_skin", "articulate_kernel<": "articula
 
 
 def short(name):
+    if "::skin_pair_kernel<" in name and ", true>" in name.split("(")[1 if name.startswith("void") else 0]:
+        return "skin_h3"  # skin_pair_kernel<kTrans, kH3 = true>: the f16x3 standalone LBS
     for k, v in KERNELS.items():
         if "::" + k in name:
             return v
