@@ -81,6 +81,9 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=None, help="override hands per GPU per step")
     ap.add_argument("--gather", action="store_true", default=None,
                     help="gather verts+joints to GPU 0 each step (default: the workload's)")
+    ap.add_argument("--event-every", type=int, default=8,
+                    help="bracket the kernels of every E-th timed step with HIP events (1 = every step; "
+                         "each timing event costs the step ~4 us, tools/debug/time_events.py)")
     ap.add_argument("--path", choices=("forward", "api", "unfused"), default="forward",
                     help="forward: mano_forward's two kernels, each bracketed by events (default); "
                          "api: one mano_forward call per step; unfused: articulate + blend + skin")
@@ -293,8 +296,14 @@ def main(argv=None):
         step()
     torch.cuda.synchronize()
 
+    # Per-kernel durations come from HIP events on the launch stream around
+    # the kernels of every E-th timed step (E = --event-every): a timing event
+    # is a release point on the stream, which costs the step ~4 us per event
+    # (0.530 vs 0.518 ms with three per step, tools/debug/time_events.py), so
+    # bracketing every step would bill the instrumentation to `value`.
+    every = max(1, min(args.event_every, args.steps // 5))  # at least 5 sampled steps
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(n_marks[args.path])]
-              for _ in range(args.steps)]
+              if i % every == 0 else None for i in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -319,7 +328,8 @@ def main(argv=None):
     timed = {"forward": {"articulate": (0, 1), "blend_skin": (1, 2)},
              "api": {"mano_forward": (0, 1)},
              "unfused": {"articulate": (0, 1), "blend": (1, 2), "skin": (2, 3)}}
-    ms = {k: span(a, b, events) for k, (a, b) in timed[args.path].items()}
+    sampled = [e for e in events if e is not None]
+    ms = {k: span(a, b, sampled) for k, (a, b) in timed[args.path].items()}
     other = {"fp32": "f16x3", "f16x3": "fp32"}[args.precision]
     ms_other = {}
     if rank == 0 and not args.no_extra:
@@ -452,6 +462,7 @@ def main(argv=None):
             "steps": args.steps,
             "warmup": args.warmup,
             "ramp": {"seconds": t_ramp, "steps": n_ramp},
+            "kernel_events": {"every": every, "sampled_steps": len(sampled)},
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
