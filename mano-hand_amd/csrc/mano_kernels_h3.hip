@@ -211,9 +211,19 @@ __device__ __forceinline__ void lbs_h3(const f16x8 (&F)[12], const f16x8& w1, co
 #ifndef MANO_H3_FULL_WAIT
 #define MANO_H3_FULL_WAIT 0
 #endif
+// MANO_H3_ABLATE (diagnostic builds; results wrong): 1 = waits without
+// s_barrier, 2 = no output stores, 4 = no LBS (v_posed stored as verts),
+// 8 = no basis DMA after the range prologue.
+#ifndef MANO_H3_ABLATE
+#define MANO_H3_ABLATE 0
+#endif
 template <int N>
 __device__ __forceinline__ void barrier_vmcnt() {
+#if MANO_H3_ABLATE & 1
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MANO_H3_FULL_WAIT ? 0 : N) : "memory");
+#else
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(MANO_H3_FULL_WAIT ? 0 : N) : "memory");
+#endif
 }
 
 #ifndef MANO_H3_NT_STORE
@@ -274,7 +284,7 @@ __global__ __launch_bounds__(64 * kH3Waves, kH3BlocksPerCU) void blend_skin_h3_k
     float* __restrict__ verts, float* __restrict__ vposed, int64_t n, int n_verts, int n_groups,
     float p_unscale, float t_unscale) {
   constexpr int kSlot = kH3GroupPieces * 64;                // f16x8 per slot (32 KB)
-  constexpr int kStores = (kVposed ? 8 : 4) * kH3TPW;       // global_store_dwordx3 per group
+  constexpr int kStores = (MANO_H3_ABLATE & 2) ? 0 : (kVposed ? 8 : 4) * kH3TPW;  // global_store_dwordx3 per group
   constexpr int kTiles = kH3Waves * kH3TPW;                 // hand tiles per block unit
   __shared__ f16x8 ring[2 * kSlot];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -327,7 +337,7 @@ __global__ __launch_bounds__(64 * kH3Waves, kH3BlocksPerCU) void blend_skin_h3_k
     barrier_vmcnt<0>();
 
     for (int grp = g0, slot = 0; grp < g1; ++grp, slot ^= 1) {
-      if (grp + 1 < g1) {
+      if (!(MANO_H3_ABLATE & 8) && grp + 1 < g1) {
         if constexpr (MANO_H3_DMA_PRIO != 0) __builtin_amdgcn_s_setprio(MANO_H3_DMA_PRIO);
         stage_group_h3(basis_h3, grp + 1, ring + (slot ^ 1) * kSlot, wave, lane);
         if constexpr (MANO_H3_DMA_PRIO != 0) __builtin_amdgcn_s_setprio(0);
@@ -377,7 +387,17 @@ __global__ __launch_bounds__(64 * kH3Waves, kH3BlocksPerCU) void blend_skin_h3_k
 #pragma unroll
           for (int r = 0; r < 4; ++r) p[t][c][r] = no_pack(p[t][c][r] * p_unscale);
         f32x4 out[3];
-        lbs_h3(F[t], w1, w2, p[t], t_unscale, tr[t], out);
+        if constexpr (MANO_H3_ABLATE & 4) {
+          out[0] = p[t][0];
+          out[1] = p[t][1];
+          out[2] = p[t][2];
+        } else {
+          lbs_h3(F[t], w1, w2, p[t], t_unscale, tr[t], out);
+        }
+        if constexpr (MANO_H3_ABLATE & 2) {
+          if (out[0][0] == 1234.5f && out[1][1] == 2345.5f) vtile[t][roff[t][0] + voff] = out[2][2];
+          continue;
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           store_out_h3(vtile[t] + (roff[t][r] + voff), f32x3{out[0][r], out[1][r], out[2][r]});
