@@ -8,6 +8,10 @@
 //   lds16     the wave stages its 16 x 192 B tile in LDS, then stores each
 //             hand row with 16-B lanes (12 lanes per 192-B row)
 //   lds16x4   the same over 4 consecutive groups (768 B per hand row)
+//   win32     rows12's units, but each hand row's 48 floats leave as 12 dwordx4
+//             from the 32-B-aligned position at or below the segment start
+//             (the sector-aligned window a carry of <= 6 floats per hand row
+//             from the previous group would give; same bytes, aligned)
 //   flat16    contiguous float4 stream (the write ceiling)
 //   copy12    rows12 read + rows12 write (skin's pattern), copy16 float4 copy
 #include <hip/hip_runtime.h>
@@ -74,6 +78,23 @@ __global__ __launch_bounds__(256) void lds16(float* __restrict__ out, long n) {
   }
 }
 
+__global__ __launch_bounds__(256) void win32(float* __restrict__ out, long n) {
+  const int lane = threadIdx.x & 63;
+  long u, ue;
+  range((n / 16) * NG, blockIdx.x * 4L + (threadIdx.x >> 6), gridDim.x * 4L, u, ue);
+  for (; u < ue; ++u) {
+    const long tile = u / NG; const int g = int(u - tile * NG);
+    const int vb = min(16 * g, NV - 16);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int idx = lane + 64 * i, h = idx / 12, c = idx - 12 * h;
+      long start = (tile * 16 + h) * VS + 3 * vb;
+      start -= start & 7;  // 32-B aligned window start
+      *reinterpret_cast<f32x4*>(out + start + 4 * c) = f32x4{float(u), float(h), float(c), 1.f};
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void flat16(f32x4* __restrict__ out, long n4) {
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += gridDim.x * 256L) out[i] = f32x4{1, 2, 3, float(i)};
 }
@@ -128,6 +149,8 @@ int main() {
     timeit(nm, W, [&] { hipLaunchKernelGGL(lds16<1>, dim3(g), dim3(256), 0, 0, b, n); });
     snprintf(nm, 64, "lds16x4 (%d blk/CU)", bpc);
     timeit(nm, W, [&] { hipLaunchKernelGGL(lds16<4>, dim3(g), dim3(256), 0, 0, b, n); });
+    snprintf(nm, 64, "win32 (%d blk/CU)", bpc);
+    timeit(nm, W, [&] { hipLaunchKernelGGL(win32, dim3(g), dim3(256), 0, 0, b, n); });
     snprintf(nm, 64, "copy12 (%d blk/CU)", bpc);
     timeit(nm, 2 * W, [&] { hipLaunchKernelGGL(copy12, dim3(g), dim3(256), 0, 0, a, b, n); });
   }
