@@ -182,7 +182,7 @@ PMC_KERNEL_NAME = {"blend_skin": "::blend_skin16_kernel<", "blend_skin_h3": "::b
                    "blend": "::blend_kernel(", "skin": "::skin_pair_kernel<", "mano_forward": "::blend_skin16_kernel<"}
 
 
-def live_traffic(args, batch, name_fragment, timeout=240):
+def live_traffic(args, batch, name_fragment, timeout=120):
     """HBM bytes per launch of the dominant kernel measured in this run: rocprofv3
     --pmc FETCH_SIZE and --pmc WRITE_SIZE as two separate passes (the counter
     budget of one pass, MI355X_MICROARCH.md) over a short child run of this bench
@@ -193,6 +193,8 @@ def live_traffic(args, batch, name_fragment, timeout=240):
     import csv
     import shutil
     import tempfile
+    if "ROCP_TOOL_LIBRARIES" in os.environ or "ROCPROF_OUTPUT_PATH" in os.environ:
+        return None, "already running under rocprofv3 (no nested profiler)"
     rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(rp):
         return None, "rocprofv3 not found"
