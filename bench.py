@@ -182,6 +182,20 @@ PMC_KERNEL_NAME = {"blend_skin": "::blend_skin16_kernel<", "blend_skin_h3": "::b
                    "blend": "::blend_kernel(", "skin": "::skin_pair_kernel<", "mano_forward": "::blend_skin16_kernel<"}
 
 
+def pmc_values(d, counter, name_fragment):
+    """Per-dispatch values of `counter` for kernels whose demangled name holds
+    `name_fragment`, from the rocprofv3 --output-format csv tree under `d`."""
+    import csv
+    vals = []
+    for root, _, files in os.walk(d):
+        for fn in files:
+            if fn.endswith("counter_collection.csv"):
+                with open(os.path.join(root, fn)) as f:
+                    vals += [float(row["Counter_Value"]) for row in csv.DictReader(f)
+                             if name_fragment in row["Kernel_Name"] and row["Counter_Name"] == counter]
+    return vals
+
+
 def live_traffic(args, batch, name_fragment, timeout=120):
     """HBM bytes per launch of the dominant kernel measured in this run: rocprofv3
     --pmc FETCH_SIZE and --pmc WRITE_SIZE as two separate passes (the counter
@@ -190,7 +204,6 @@ def live_traffic(args, batch, name_fragment, timeout=120):
     region.  hbm_read = 2 x FETCH_SIZE x 1 KB (gfx950 counts half of a wide
     coalesced read, same guide), hbm_write = WRITE_SIZE x 1 KB, averaged over the
     kernel's dispatches.  Returns (bytes, detail) or (None, reason)."""
-    import csv
     import shutil
     import tempfile
     if "ROCP_TOOL_LIBRARIES" in os.environ or "ROCPROF_OUTPUT_PATH" in os.environ:
@@ -213,13 +226,7 @@ def live_traffic(args, batch, name_fragment, timeout=120):
                                capture_output=True, text=True, timeout=timeout, env=env, cwd="/tmp")
             if r.returncode != 0:
                 return None, f"rocprofv3 --pmc {counter} rc {r.returncode}: {r.stderr[-300:]}"
-            vals = []
-            for root, _, files in os.walk(d):
-                for fn in files:
-                    if fn.endswith("counter_collection.csv"):
-                        with open(os.path.join(root, fn)) as f:
-                            vals += [float(row["Counter_Value"]) for row in csv.DictReader(f)
-                                     if name_fragment in row["Kernel_Name"] and row["Counter_Name"] == counter]
+            vals = pmc_values(d, counter, name_fragment)
             if not vals:
                 return None, f"no {counter} rows for {name_fragment}"
             kb[counter] = sum(vals) / len(vals)

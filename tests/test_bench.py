@@ -72,3 +72,23 @@ def test_traffic_lookup(tmp_path):
 
 def test_cpu_share_bounded():
     assert 1 <= bench.cpu_share() <= 16
+
+
+def test_pmc_values_parse(tmp_path):
+    """bench.py's live roofline.traffic reads rocprofv3's counter CSV: per-dispatch
+    values of one counter for the dominant kernel only."""
+    import bench
+    sub = tmp_path / "host" / "123"
+    sub.mkdir(parents=True)
+    hdr = "Correlation_Id,Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value\n"
+    rows = [
+        '1,1,"void mano::(anonymous namespace)::blend_skin16_kernel<false, false>(float const*)",FETCH_SIZE,100\n',
+        '2,2,"void mano::(anonymous namespace)::articulate_kernel<false>(float const*)",FETCH_SIZE,7\n',
+        '3,3,"void mano::(anonymous namespace)::blend_skin16_kernel<false, false>(float const*)",FETCH_SIZE,300\n',
+        '4,3,"void mano::(anonymous namespace)::blend_skin16_kernel<false, false>(float const*)",WRITE_SIZE,9\n',
+    ]
+    (sub / "p_counter_collection.csv").write_text(hdr + "".join(rows))
+    frag = bench.PMC_KERNEL_NAME["blend_skin"]
+    assert bench.pmc_values(str(tmp_path), "FETCH_SIZE", frag) == [100.0, 300.0]
+    assert bench.pmc_values(str(tmp_path), "WRITE_SIZE", frag) == [9.0]
+    assert bench.pmc_values(str(tmp_path), "FETCH_SIZE", bench.PMC_KERNEL_NAME["blend_skin_h3"]) == []

@@ -22,7 +22,7 @@ LIB = os.path.join(REPO, "mano-hand_amd", "mano_amd", "libmano_hip.so")
 LLVM = "/opt/rocm/llvm/bin"
 WATCH = {
     "packed_fp32": re.compile(r"\bv_pk_(fma|mul|add)_f32\b"),
-    "scalar_store": re.compile(r"\b(s_store_dword\w*|s_buffer_store\w*|s_scratch_store\w*|s_dcache_wb\w*|s_dcache_discard\w*)\b"),
+    "scalar_store": re.compile(r"\b(s_store_dword\w*|s_buffer_store\w*|s_scratch_store\w*|s_dcache_wb\w*|s_dcache_discard\w*|s_atomic_\w*|s_buffer_atomic_\w*)\b"),
 }
 
 
