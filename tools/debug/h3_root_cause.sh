@@ -8,7 +8,7 @@
 set -eu
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 PKG=mano-hand_amd
-SRCS="$PKG/csrc/mano_abi.hip $PKG/csrc/mano_comm.hip $PKG/csrc/mano_pack.cpp $PKG/csrc/mano_kernels.hip $PKG/csrc/mano_kernels_h3.hip $PKG/csrc/mano_skin_quad.hip"
+SRCS="$PKG/csrc/mano_abi.hip $PKG/csrc/mano_comm.hip $PKG/csrc/mano_pack.cpp $PKG/csrc/mano_articulate.hip $PKG/csrc/mano_kernels.hip $PKG/csrc/mano_kernels_h3.hip $PKG/csrc/mano_skin_quad.hip"
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ldl"
 if [ "${1:-}" = build ]; then
   /opt/rocm/bin/hipcc $FLAGS -DMANO_H3_NO_PACK=0 -o $PKG/mano_amd/libmano_hip_pack.so $SRCS
