@@ -342,8 +342,11 @@ __device__ __forceinline__ void bs_stamp(int slot, unsigned long long v) {
 }
 #endif
 
+#ifndef MANO_BS_BLOCKS_PER_CU
+#define MANO_BS_BLOCKS_PER_CU 3  // resident blocks per CU (diagnostic builds: 1, 2, 4)
+#endif
 template <bool kTrans, bool kVposed>
-__global__ __launch_bounds__(256, 3) void blend_skin16_kernel(
+__global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kernel(
     const float* __restrict__ features, const float* __restrict__ transforms,
     const float* __restrict__ basis16, const float* __restrict__ wfrag16,
     const float* __restrict__ trans, float* __restrict__ verts, float* __restrict__ vposed,
@@ -677,10 +680,7 @@ namespace {
 // occupancy API only caps that, because it reads one block per CU high for
 // kernels using 97-112 SGPRs on gfx950 (MI355X_MICROARCH.md, correctness
 // boundaries).
-#ifndef MANO_BS_BLOCKS_PER_CU
-#define MANO_BS_BLOCKS_PER_CU 3  // diagnostic builds: fewer resident blocks per CU
-#endif
-constexpr int kBlendSkinBlocksPerCU = MANO_BS_BLOCKS_PER_CU;  // 168 VGPRs: 3 waves per SIMD
+constexpr int kBlendSkinBlocksPerCU = MANO_BS_BLOCKS_PER_CU;  // 142 VGPRs: 3 waves per SIMD
 constexpr int kSkinBlocksPerCU = MANO_SPAN_BLOCKS_PER_CU;  // skin_span
 
 template <class Kernel>
