@@ -197,8 +197,33 @@ __global__ __launch_bounds__(256) void articulate_kernel(
   __shared__ float js_s[kJoints * 3 * kShape];
   float* xs = reinterpret_cast<float*>(xs4);
   const int tid = threadIdx.x;
-  for (int i = tid; i < kJoints * 3 * kShape; i += 256) js_s[i] = joint_shape[i];
-  if (tid < kJoints * 3) jt_s[tid] = joint_template[tid];
+  const int j = tid & (kJoints - 1);
+  const int hl = tid >> 4;
+  const int64_t h0 = int64_t(blockIdx.x) * 16;
+  const int64_t h = min(h0 + hl, n - 1);  // tail lanes repeat the last hand
+  const bool valid = h0 + hl < n;
+
+  // Every global load of the prologue is issued before the first LDS write
+  // (the lane's pose and betas, then the block's regressor fold): written as
+  // load-then-store loops, hipcc waited for each load before its ds_write --
+  // three serial round trips before any arithmetic.
+  float aa[3] = {0.f, 0.f, 0.f};
+  if constexpr (!kFromPca) {
+    const float* p = pose + h * (kJoints * 3) + 3 * j;
+    aa[0] = p[0];
+    aa[1] = p[1];
+    aa[2] = p[2];
+  }
+  float beta[kShape];
+#pragma unroll
+  for (int s = 0; s < kShape; ++s) beta[s] = betas[h * betas_stride + s];
+  constexpr int kJs = kJoints * 3 * kShape;  // 480 = 256 + 224
+  const float js0 = joint_shape[tid];
+  const float js1 = tid + 256 < kJs ? joint_shape[tid + 256] : 0.f;
+  const float jt0 = tid < kJoints * 3 ? joint_template[tid] : 0.f;
+  js_s[tid] = js0;
+  if (tid + 256 < kJs) js_s[tid + 256] = js1;
+  if (tid < kJoints * 3) jt_s[tid] = jt0;
   const float* basis_s = nullptr;
   const float* mean_s = nullptr;
   if constexpr (kFromPca) {
@@ -209,28 +234,14 @@ __global__ __launch_bounds__(256) void articulate_kernel(
     mean_s = pb_s + kPca * kPca;
   }
   __syncthreads();
-  const int j = tid & (kJoints - 1);
-  const int hl = tid >> 4;
-  const int64_t h0 = int64_t(blockIdx.x) * 16;
-  const int64_t h = min(h0 + hl, n - 1);  // tail lanes repeat the last hand
-  const bool valid = h0 + hl < n;
 
-  float aa[3];
   if constexpr (kFromPca) {
     pca_joint_pose(pca, basis_s, mean_s, h, j, aa);
     if (valid && pca.pose_out) {
 #pragma unroll
       for (int c = 0; c < 3; ++c) pca.pose_out[h * (kJoints * 3) + 3 * j + c] = aa[c];
     }
-  } else {
-    const float* p = pose + h * (kJoints * 3) + 3 * j;
-    aa[0] = p[0];
-    aa[1] = p[1];
-    aa[2] = p[2];
   }
-  float beta[kShape];
-#pragma unroll
-  for (int s = 0; s < kShape; ++s) beta[s] = betas[h * betas_stride + s];
   const int par = parents[j];
   const int src = ((tid & 63) & ~(kJoints - 1)) + (par < 0 ? 0 : par);
   float rm[9], J[3], t[3], Aj[12];
