@@ -1,9 +1,11 @@
 """The C-ABI library loads, exports every symbol include/mano_hip.h declares,
 and rejects bad arguments with status codes -- all without touching a GPU."""
 import ctypes
+import os
 
 import pytest
 
+from conftest import REPO
 from mano_amd import _abi
 
 
@@ -92,3 +94,15 @@ def test_forward_pca_and_comm_argument_checks():
     assert lib.mano_comm_destroy(None) == _abi.MANO_OK
     assert lib.mano_gather(None, None, 0, None, None, 0, None) == _abi.MANO_EINVAL
     assert lib.mano_comm_unique_id(None) == _abi.MANO_EINVAL
+
+
+def test_makefile_matches_build_flags():
+    """`make -C mano-hand_amd` and __graft_entry__.build() compile every source
+    with the same per-source flags (the max-ILP scheduler, the MFMA VGPR form)."""
+    import re
+    import __graft_entry__ as g
+    mk = open(os.path.join(REPO, "mano-hand_amd", "Makefile")).read()
+    srcs = re.search(r"^SRCS := (.*)$", mk, re.M).group(1).split()
+    assert [os.path.basename(x) for x in srcs] == [os.path.basename(x) for x in g.SRCS]
+    extra = {m.group(1): m.group(2).split() for m in re.finditer(r"^\$\(OBJDIR\)/(\S+)\.o: EXTRA := (.*)$", mk, re.M)}
+    assert extra == {k: v for k, v in g.SRC_FLAGS.items()}
