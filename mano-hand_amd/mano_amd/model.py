@@ -125,7 +125,10 @@ class ManoHip:
         rule for concurrent calls), and each workspace is allocated ON its
         stream, so when it grows the caching allocator hands the old block out
         again only in that stream's order -- never while a queued launch on the
-        stream may still read it."""
+        stream may still read it.  A grown workspace starts with the old one's
+        contents (same offsets, workspace_layout depends on n only), so the
+        X rows and transforms of a preceding forward() stay valid for the stage
+        calls that need the larger, unfused layout."""
         lib = _abi.lib()
         need = int(lib.mano_forward_workspace_bytes(self._h, n) if forward_only
                    else lib.mano_workspace_bytes(self._h, n))
@@ -133,10 +136,21 @@ class ManoHip:
         key = s.cuda_stream
         ws = self._ws.get(key)
         if ws is None or ws.numel() < need + 256:
+            old = ws
             with torch.cuda.stream(s):
                 ws = torch.empty(max(need, 256) + 256, dtype=torch.uint8, device=self.device)
+                if old is not None:
+                    src, dst = self._aligned_view(old), self._aligned_view(ws)
+                    k = min(src.numel(), dst.numel())
+                    dst[:k].copy_(src[:k])
             self._ws[key] = ws
         return ws
+
+    @staticmethod
+    def _aligned_view(ws: torch.Tensor) -> torch.Tensor:
+        """The 256-B-aligned part of a workspace tensor (what the ABI is given)."""
+        base = ws.data_ptr()
+        return ws[((base + 255) & ~255) - base:]
 
     def _ws_args(self, n, forward_only: bool = False, stream=None):
         ws = self.workspace(n, forward_only, stream)

@@ -176,3 +176,47 @@ def test_standalone_skin_on_exact_vposed(h3, dev, params):
     h3.stage_skin(B, v, rest_verts=vp)
     torch.cuda.synchronize()
     check({"verts": v}, mano_oracle.forward(params, host(betas), host(pose)), "skin_h3")
+
+
+def test_rest_verts_launches_deterministic(h3, dev):
+    """The instantiation that once returned wrong hand-row-14/15 x coordinates
+    under load (blend_skin_h3 with rest_verts and trans): 40
+    back-to-back launches at 65,536 hands give the same bits as the first,
+    and the fused LBS equals the standalone one on that v_posed."""
+    B = 65536
+    inp = h3.synthetic_inputs(77, 0, B, trans=True)
+    betas, pose, trans = inp["betas"], inp["pose"], inp["trans"]
+    ref_v = torch.empty((B, 778, 3), device=dev)
+    ref_p = torch.empty_like(ref_v)
+    h3.stage_articulate(betas, pose, trans)
+    h3.stage_blend_skin(B, ref_v, rest_verts=ref_p, trans=trans)
+    v = torch.empty_like(ref_v)
+    p = torch.empty_like(ref_p)
+    bad = 0
+    for _ in range(40):
+        h3.stage_blend_skin(B, v, rest_verts=p, trans=trans)
+        bad += int(not torch.equal(v, ref_v)) + int(not torch.equal(p, ref_p))
+    torch.cuda.synchronize()
+    assert bad == 0, f"{bad} of 80 outputs differ from the first launch"
+    s = torch.empty_like(ref_v)
+    h3.stage_skin(B, s, rest_verts=ref_p, trans=trans)
+    torch.cuda.synchronize()
+    assert torch.equal(s, ref_v)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "f16x3"])
+def test_forward_then_stage_blend_skin(params, dev, precision):
+    """A stage call after forward() reuses forward's X rows and transforms even
+    when it grows the stream's workspace to the unfused layout (the grown
+    workspace starts with the old contents), bit for bit."""
+    from mano_amd import ManoHip
+    m = ManoHip(params, device=0, precision=precision)
+    B = 4096
+    inp = m.synthetic_inputs(78, 0, B, trans=True)
+    ref = m.forward(inp["betas"], inp["pose"], inp["trans"], rest_verts=True)
+    v = torch.empty((B, 778, 3), device=dev)
+    p = torch.empty_like(v)
+    m.stage_blend_skin(B, v, rest_verts=p, trans=inp["trans"])
+    torch.cuda.synchronize()
+    assert torch.equal(v, ref["verts"]) and torch.equal(p, ref["rest_verts"])
+    m.close()
