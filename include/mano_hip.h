@@ -121,6 +121,9 @@ int mano_forward(const mano_model* model, int64_t n_hands,
 
 /* The forward pass as separate kernels, callable one at a time (workspace of
  * mano_workspace_bytes), so each can be timed and its intermediates checked.
+ * blend, skin and blend_skin read the X rows and transforms that the last
+ * articulate (or mano_forward) on the same n_hands left in the same
+ * workspace; the offsets depend on n_hands only (mano_workspace_offsets). */
  *  articulate: Rodrigues (mano_np.py:117-148) + joint regression (:83) +
  *              pose features (:87-91) + kinematic chain (:96-104) +
  *              rest-pose removal (:106-110).
