@@ -98,6 +98,10 @@ def parse(argv=None):
     ap.add_argument("--cpu-procs", type=int, default=None,
                     help="CPU-baseline processes (default: this box's CPU share, at most 16)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dump-gather", default=None,
+                    help="(tests) rank 0 saves GPU 0's gathered verts / joints to this .npz after timing")
+    ap.add_argument("--no-check", action="store_true",
+                    help="skip the correctness leg (sampled hands of the timed step vs the oracle)")
     ap.add_argument("--no-extra", action="store_true", help="skip the untimed other-path kernel table")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                     help="committed rocprofv3 --pmc summary: roofline.traffic when the live passes fail")
@@ -153,6 +157,79 @@ def cpu_baseline(procs, seconds):
                         "sample": f"{bt['hands']} hands in 256-hand float64 BLAS-GEMM batches "
                                   f"(oracle/cpu_baseline.py forward_gemm) in {procs} processes x "
                                   f"{bt['seconds']:.1f} s, OMP_NUM_THREADS=1"}}
+
+
+def sample_indices(B, n_random=48, seed=0):
+    """First, last, tile-boundary (16-hand tiles, 64-hand quads), middle and
+    random hands of a B-hand shard."""
+    edges = [0, 1, 15, 16, 63, 64, B // 2 - 1, B // 2, B - 65, B - 64, B - 17, B - 16, B - 2, B - 1]
+    rnd = np.random.default_rng(seed).integers(0, B, n_random)
+    return np.unique(np.clip(np.concatenate([edges, rnd]), 0, B - 1))
+
+
+def check_sample(model, seed, first, B, betas, pose, trans, verts, joints, model_path, with_trans,
+                 tol=1e-5):
+    """Max |GPU - oracle| over sampled hands of the timed step's outputs: the
+    hands' inputs and outputs go to an .npz, the float64 oracle runs in a child
+    process (oracle/check_sample.py), so this process never imports oracle/."""
+    import tempfile
+    import torch
+    idx = sample_indices(B)
+    ti = torch.as_tensor(idx, device=verts.device)
+    f = lambda t: t.index_select(0, ti).cpu().numpy()  # noqa: E731
+    arrays = {"index": idx + first, "betas": f(betas), "pose": f(pose), "verts": f(verts),
+              "joints": f(joints),
+              "model": np.array(os.path.abspath(model_path) if model_path else "synthetic:0")}
+    if with_trans and trans is not None:
+        arrays["trans"] = f(trans)
+    fd, path = tempfile.mkstemp(prefix="mano_check_", suffix=".npz", dir="/tmp")
+    os.close(fd)
+    try:
+        np.savez(path, **arrays)
+        r = subprocess.run([sys.executable, os.path.join(REPO, "oracle", "check_sample.py"), path],
+                           capture_output=True, text=True, timeout=300)
+        if r.returncode != 0:
+            return {"error": r.stderr[-500:]}
+        res = json.loads(r.stdout.strip().splitlines()[-1])
+    finally:
+        os.unlink(path)
+    res["tolerance_m"] = tol
+    res["pass"] = bool(res["finite"] and res["max_abs_err_verts"] <= tol and res["max_abs_err_joints"] <= tol)
+    res["reference"] = ("oracle/mano_oracle.py float64 (mano_np.py:79-115, pinned to the reference's "
+                        "outputs by tests/test_oracle_golden.py), the last timed step's outputs")
+    return res
+
+
+def check_gather(model, seed, B, world, gv, gj, with_trans, per_rank=64):
+    """GPU 0's gathered buffers vs a local forward: from every rank's range
+    [r B, (r + 1) B) the first 16, last 16 and a random run of 32 hands are
+    regenerated by global index and forwarded on this GPU; the rows must equal
+    gv / gj bit for bit (hands are independent, mano_np.py:79-115)."""
+    import torch
+    rng = np.random.default_rng(1)
+    bad, n, ranks_bad = 0, 0, []
+    for r in range(world):
+        k = min(16, B)
+        runs = [(0, k), (max(0, B - k), k)]
+        if B > 32:
+            runs.append((int(rng.integers(0, B - 32)), 32))
+        wrong = 0
+        for off, cnt in runs:
+            g0 = r * B + off
+            inp = model.synthetic_inputs(seed, g0, cnt, trans=with_trans)
+            out = model.forward(inp["betas"], inp["pose"], inp.get("trans"), joints=True)
+            dv = (out["verts"] != gv[g0:g0 + cnt]).flatten(1).any(1)
+            dj = (out["joints"] != gj[g0:g0 + cnt]).flatten(1).any(1)
+            wrong += int((dv | dj).sum())
+            n += cnt
+        bad += wrong
+        if wrong:
+            ranks_bad.append(r)
+    torch.cuda.synchronize()
+    return {"ranks": world, "hands_checked": n, "hands_wrong": bad, "ranks_wrong": ranks_bad,
+            "bit_exact": bad == 0,
+            "method": "rank 0 regenerates each rank's first 16, last 16 and 32 random consecutive hands "
+                      "by global index, forwards them locally, compares with GPU 0's gathered verts / joints"}
 
 
 def load_traffic(path, kernel, batch):
@@ -213,7 +290,7 @@ def live_traffic(args, batch, name_fragment, timeout=120):
         return None, "rocprofv3 not found"
     child = [sys.executable, os.path.abspath(__file__), "--workload", args.workload, "--batch", str(batch),
              "--precision", args.precision, "--path", args.path, "--steps", "3", "--warmup", "1",
-             "--ramp-seconds", "0", "--no-cpu", "--no-extra", "--no-live-pmc"]
+             "--ramp-seconds", "0", "--no-cpu", "--no-extra", "--no-live-pmc", "--no-check"]
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK",
                         "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
@@ -309,9 +386,9 @@ def main(argv=None):
     if gather and world > 1:
         if args.backend == "nccl":
             gatherer = AbiGather(local_dev)
-            if rank == 0:  # GPU 0's assembled buffers, allocated once
-                gv = torch.empty((B * world, V, 3), device=dev)
-                gj = torch.empty((B * world, 16, 3), device=dev)
+        if rank == 0:  # GPU 0's assembled buffers (mano_gather's layout), allocated once
+            gv = torch.empty((B * world, V, 3), device=dev)
+            gj = torch.empty((B * world, 16, 3), device=dev)
 
     # Launch sequence of one step; `marks` get an event after each kernel.
     # "forward" issues exactly mano_forward's two launches (articulate, then
@@ -346,8 +423,12 @@ def main(argv=None):
             if gatherer is not None:  # RCCL over xGMI, peer -> GPU 0 sends
                 gatherer.gather(verts, B * world, root=0, out=gv)
                 gatherer.gather(joints, B * world, root=0, out=gj)
-            else:  # gloo rehearsal: the joints through the host
-                gather_to_root(joints.cpu(), B * world, root=0)
+            else:  # gloo rehearsal: verts + joints through the host into the same gv / gj layout
+                fv = gather_to_root(verts.cpu(), B * world, root=0)
+                fj = gather_to_root(joints.cpu(), B * world, root=0)
+                if rank == 0:
+                    gv.copy_(fv)
+                    gj.copy_(fj)
 
     # Clock ramp, then the untimed warmup.
     t_ramp = time.perf_counter()
@@ -533,6 +614,19 @@ def main(argv=None):
         roof["hands_per_launch"] = B
         roof["timed_in_region"] = dominant in in_path
 
+    # Correctness of the timed outputs (the last timed step's verts / joints):
+    # sampled hands vs the float64 oracle in a child process, and at N > 1 with
+    # a gather, GPU 0's assembled buffers vs a local forward of hands
+    # regenerated by global index from every rank's range.
+    correctness, gather_check = None, None
+    if rank == 0 and not args.no_check:
+        correctness = check_sample(model, wl["seed"], rank * B, B, betas, pose, trans, verts, joints,
+                                   args.model, with_trans)
+    if rank == 0 and gv is not None:
+        gather_check = check_gather(model, wl["seed"], B, world, gv, gj, with_trans)
+        if args.dump_gather:
+            np.savez(args.dump_gather, verts=gv.cpu().numpy(), joints=gj.cpu().numpy())
+
     if rank == 0:
         total = B * world * args.steps
         line = {
@@ -562,7 +656,10 @@ def main(argv=None):
                        "parallelism": f"dp{world}"},
             "roofline": roof,
             "kernels": kernels,
+            "correctness": correctness,
         }
+        if gather_check is not None:
+            line["gather_check"] = gather_check
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(args.cpu_procs or cpu_share(), args.cpu_seconds)
         print(json.dumps(line), flush=True)

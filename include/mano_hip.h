@@ -16,7 +16,8 @@
  *     every pointer given to the forward / stage / helper calls is a DEVICE
  *     pointer owned by the caller, on the model's device.
  *   - Launches are asynchronous on `stream` (a hipStream_t; NULL = the
- *     device's null stream).  Nothing blocks except model create/destroy.
+ *     device's null stream).  Nothing blocks except model create/destroy,
+ *     mano_model_device_status, mano_synchronize and NULL-stream mano_memcpy.
  *   - A model handle is bound to one device.  Calls on one handle may come
  *     from several host threads only if they use distinct workspaces.
  *   - Layouts are the reference's, row-major float32:
@@ -93,6 +94,18 @@ int mano_model_destroy(mano_model* model);
 /* Vertex count and device of a model. */
 int mano_model_info(const mano_model* model, int32_t* n_verts, int32_t* device);
 
+/* Device status word of a model: MANO_DEVICE_* bits raised by kernels since
+ * the last clear.  Waits for every launch on the model's device first
+ * (hipDeviceSynchronize), reads the word into *status and, with `clear`
+ * non-zero, resets it.  A non-zero word means some launch's outputs are not
+ * valid:
+ *   MANO_DEVICE_SKIN_HANDOFF_TIMEOUT  the standalone LBS (mano_stage_skin) lost
+ *     a hand-over between its memory and compute waves (a bounded LDS wait
+ *     gave up); the verts of the units it could not confirm were not
+ *     written. */
+#define MANO_DEVICE_SKIN_HANDOFF_TIMEOUT 1
+int mano_model_device_status(const mano_model* model, int32_t* status, int32_t clear);
+
 /* Device workspace (bytes) for n_hands: `mano_workspace_bytes` covers every
  * call (the unfused stages keep v_posed in it); `mano_forward_workspace_bytes`
  * only what mano_forward / articulate / blend_skin use (X rows + transforms,
@@ -123,7 +136,7 @@ int mano_forward(const mano_model* model, int64_t n_hands,
  * mano_workspace_bytes), so each can be timed and its intermediates checked.
  * blend, skin and blend_skin read the X rows and transforms that the last
  * articulate (or mano_forward) on the same n_hands left in the same
- * workspace; the offsets depend on n_hands only (mano_workspace_offsets). */
+ * workspace; the offsets depend on n_hands only (mano_workspace_offsets).
  *  articulate: Rodrigues (mano_np.py:117-148) + joint regression (:83) +
  *              pose features (:87-91) + kinematic chain (:96-104) +
  *              rest-pose removal (:106-110).

@@ -94,7 +94,7 @@ int set_error(int code, const char* msg) {
 
 extern "C" {
 
-int mano_abi_version(void) { return 2; }
+int mano_abi_version(void) { return 3; }
 
 const char* mano_last_error(void) { return g_last_error.c_str(); }
 
@@ -135,7 +135,7 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
 
   // ---- one device block, 256-B aligned sub-arrays ----
   struct Part { const void* src; size_t bytes; size_t off; };
-  enum { kBasis, kWeights, kJt, kJs, kParents, kDepth, kPcaB, kPcaM, kZeros, kBasis16, kW16, kBasisH3, kNParts };
+  enum { kBasis, kWeights, kJt, kJs, kParents, kDepth, kPcaB, kPcaM, kZeros, kStatus, kBasis16, kW16, kBasisH3, kNParts };
   std::vector<Part> parts(kNParts);
   parts[kBasis] = {hm.tiles.data(), hm.tiles.size() * 4, 0};
   parts[kWeights] = {hm.weights.data(), hm.weights.size() * 4, 0};
@@ -146,6 +146,7 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   parts[kPcaB] = {hm.pca.data(), hm.pca.size() * 4, 0};
   parts[kPcaM] = {hm.pmean.data(), hm.pmean.size() * 4, 0};
   parts[kZeros] = {zeros.data(), zeros.size() * 4, 0};
+  parts[kStatus] = {zeros.data(), 4, 0};
   parts[kBasis16] = {hm.b16.data(), hm.b16.size() * 4, 0};
   parts[kW16] = {hm.w16.data(), hm.w16.size() * 4, 0};
   parts[kBasisH3] = {hm.bh3.data(), hm.bh3.size() * 2, 0};
@@ -183,6 +184,7 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   m->dm.pca_basis = at(kPcaB);
   m->dm.pca_mean = at(kPcaM);
   m->dm.zeros = at(kZeros);
+  m->dm.status = reinterpret_cast<int32_t*>(at(kStatus));
   m->dm.basis16 = at(kBasis16);
   m->dm.wfrag16 = at(kW16);
   m->dm.basis_h3 = reinterpret_cast<uint16_t*>(at(kBasisH3));
@@ -232,6 +234,26 @@ int mano_model_get_precision(const mano_model* m, int32_t* precision) {
   if (int rc = check_model(m)) return rc;
   if (!precision) return fail(MANO_EINVAL, "precision is NULL");
   *precision = m->dm.precision;
+  return MANO_OK;
+}
+
+int mano_model_device_status(const mano_model* m, int32_t* status, int32_t clear) {
+  g_last_error.clear();
+  if (int rc = check_model(m)) return rc;
+  if (!status) return fail(MANO_EINVAL, "status is NULL");
+  DeviceGuard guard(m->device);
+  if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
+  int32_t word = 0;
+  e = hipMemcpy(&word, m->dm.status, sizeof(word), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail(e, "hipMemcpy(status)");
+  if (clear && word != 0) {
+    e = hipMemset(m->dm.status, 0, sizeof(word));
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) return hip_fail(e, "hipMemset(status)");
+  }
+  *status = word;
   return MANO_OK;
 }
 

@@ -22,6 +22,7 @@ struct DeviceModel {
   float* pca_basis;     // [45][45]
   float* pca_mean;      // [45]
   float* zeros;         // [64] zero vector (stand-in operand for an absent trans)
+  int32_t* status;      // device status word: MANO_DEVICE_* bits raised by kernels
   float* basis16;       // [n_groups16][3][kTile16Floats]
   float* wfrag16;       // [n_groups16][kWFrag16Floats]
   uint16_t* basis_h3;   // [n_groups16][kH3GroupHalves] f16 bits (f16x3 mode)
@@ -80,7 +81,7 @@ hipError_t launch_skin(const DeviceModel& m, int64_t n, const float* transforms,
                        const float* vposed, const float* trans, float* verts,
                        hipStream_t stream);
 // The 4-hand-unit fp32 LBS (mano_skin_quad.hip); launch_skin uses it when
-// skin_quad_supported(m) (16 <= V <= 1024).
+// skin_quad_supported(m) (16 <= V <= 832: W of every group resident in LDS).
 bool skin_quad_supported(const DeviceModel& m);
 hipError_t launch_skin_quad(const DeviceModel& m, int64_t n, const float* transforms,
                             const float* vposed, const float* trans, float* verts,

@@ -617,36 +617,39 @@ __global__ __launch_bounds__(256) void synthetic_inputs_kernel(
     uint32_t k0, uint32_t k1, int64_t first, int64_t n, float beta_sigma, float pose_sigma,
     float trans_range, float* __restrict__ betas, float* __restrict__ pose,
     float* __restrict__ trans) {
-  const int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x;
-  const int64_t h = idx >> 4;
-  const int b = int(idx & 15);
-  if (h >= n) return;
-  const uint64_t g = uint64_t(first + h);
-  uint32_t w[4] = {uint32_t(g), uint32_t(g >> 32), uint32_t(b), 0u};
-  philox4x32_10(w, k0, k1);
+  // Grid-stride over the n * 16 (hand, block) lanes: the grid is bounded
+  // (launch_synthetic_inputs), any n up to the ABI's 2^30 hands.
+  for (int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x; idx < n * 16;
+       idx += int64_t(gridDim.x) * 256) {
+    const int64_t h = idx >> 4;
+    const int b = int(idx & 15);
+    const uint64_t g = uint64_t(first + h);
+    uint32_t w[4] = {uint32_t(g), uint32_t(g >> 32), uint32_t(b), 0u};
+    philox4x32_10(w, k0, k1);
 #pragma unroll
-  for (int pr = 0; pr < 2; ++pr) {
-    const int e = 4 * b + 2 * pr;  // element index of the pair's first member
-    float v[2];
-    if (e < 58) {
-      const float r = sqrtf(-2.0f * logf(unit_open(w[2 * pr])));
-      float s, c;
-      sincospif(2.0f * unit_open(w[2 * pr + 1]), &s, &c);
-      v[0] = r * c;
-      v[1] = r * s;
-    } else {
-      v[0] = 2.0f * unit_open(w[2 * pr]) - 1.0f;
-      v[1] = 2.0f * unit_open(w[2 * pr + 1]) - 1.0f;
-    }
+    for (int pr = 0; pr < 2; ++pr) {
+      const int e = 4 * b + 2 * pr;  // element index of the pair's first member
+      float v[2];
+      if (e < 58) {
+        const float r = sqrtf(-2.0f * logf(unit_open(w[2 * pr])));
+        float s, c;
+        sincospif(2.0f * unit_open(w[2 * pr + 1]), &s, &c);
+        v[0] = r * c;
+        v[1] = r * s;
+      } else {
+        v[0] = 2.0f * unit_open(w[2 * pr]) - 1.0f;
+        v[1] = 2.0f * unit_open(w[2 * pr + 1]) - 1.0f;
+      }
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int el = e + q;
-      if (el < kShape) {
-        if (betas) betas[h * kShape + el] = beta_sigma * v[q];
-      } else if (el < 58) {
-        if (pose) pose[h * (kJoints * 3) + (el - kShape)] = pose_sigma * v[q];
-      } else if (el < 61) {
-        if (trans) trans[h * 3 + (el - 58)] = trans_range * v[q];
+      for (int q = 0; q < 2; ++q) {
+        const int el = e + q;
+        if (el < kShape) {
+          if (betas) betas[h * kShape + el] = beta_sigma * v[q];
+        } else if (el < 58) {
+          if (pose) pose[h * (kJoints * 3) + (el - kShape)] = pose_sigma * v[q];
+        } else if (el < 61) {
+          if (trans) trans[h * 3 + (el - 58)] = trans_range * v[q];
+        }
       }
     }
   }
@@ -658,7 +661,8 @@ hipError_t launch_synthetic_inputs(uint64_t seed, int64_t first, int64_t n, floa
                                    float pose_sigma, float trans_range, float* betas, float* pose,
                                    float* trans, hipStream_t stream) {
   const int64_t threads = n * 16;
-  hipLaunchKernelGGL(synthetic_inputs_kernel, dim3(unsigned((threads + 255) / 256)), dim3(256), 0,
+  const int64_t blocks = std::min<int64_t>((threads + 255) / 256, int64_t(1) << 20);  // grid-stride beyond
+  hipLaunchKernelGGL(synthetic_inputs_kernel, dim3(unsigned(blocks)), dim3(256), 0,
                      stream, uint32_t(seed), uint32_t(seed >> 32), first, n, beta_sigma, pose_sigma,
                      trans_range, betas, pose, trans);
   return hipGetLastError();

@@ -11,6 +11,8 @@
 #include <string>
 #include <vector>
 
+#include "mano_diag.h"
+
 #if !defined(__HIP__) && !defined(__host__)
 #define __host__
 #define __device__

@@ -42,6 +42,7 @@
 #include <algorithm>
 #include <cstddef>
 
+#include "../../include/mano_hip.h"
 #include "mano_internal.h"
 
 namespace mano {
@@ -456,8 +457,15 @@ __device__ __forceinline__ unsigned lds_addr(const int* p) {
   typedef const __attribute__((address_space(3))) int* lds_ptr;
   return unsigned(reinterpret_cast<uintptr_t>((lds_ptr)p));  // generic -> LDS address (32 bit)
 }
-// Bounded: false after ~2^20 polls (tens of ms), and the caller then stops
-// -- a lost hand-over ends the kernel with wrong results, never hangs it.
+// Bounded: false after kPairPollLimit polls (2^20: tens of ms), and the
+// caller then stops -- a lost hand-over never hangs the kernel; it raises
+// MANO_DEVICE_SKIN_HANDOFF_TIMEOUT in the model's device status word
+// (mano_model_device_status), and the memory wave drops the stores of every
+// unit it could not confirm as skinned, so no un-skinned row reaches verts.
+#ifndef MANO_PAIR_POLL_LIMIT
+#define MANO_PAIR_POLL_LIMIT (1 << 20)  // diagnostic builds: tiny limits force the timeout path
+#endif
+constexpr int kPairPollLimit = MANO_PAIR_POLL_LIMIT;
 #ifndef MANO_PAIR_SLEEP_MEM
 #define MANO_PAIR_SLEEP_MEM 1  // s_sleep between the memory wave's polls (0 = none)
 #endif
@@ -467,13 +475,18 @@ __device__ __forceinline__ unsigned lds_addr(const int* p) {
 template <int kSleep = 1>
 __device__ __forceinline__ bool pair_wait_ge(const int* flag, int target) {
   const unsigned a = lds_addr(flag);
-  for (int it = 0; it < (1 << 20); ++it) {
+  for (int it = 0; it < kPairPollLimit; ++it) {
     int x;
     asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(x) : "v"(a) : "memory");
     if (__builtin_amdgcn_readfirstlane(x) >= target) return true;
     if constexpr (kSleep > 0) __builtin_amdgcn_s_sleep(kSleep);
   }
   return false;
+}
+// A hand-over wait gave up: one lane ORs the bit into the device status word
+// (a vector global atomic; read back by mano_model_device_status).
+__device__ __forceinline__ void raise_status(int* status, int bit) {
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or(status, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void pair_signal(int* flag, int value) {
   // the slot's LDS writes have landed before the counter moves
@@ -538,7 +551,8 @@ template <bool kTrans, bool kH3 = false>
 __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     const float* __restrict__ transforms, const float* __restrict__ wfrag16,
     const float* __restrict__ vposed, const float* __restrict__ trans, float* __restrict__ verts,
-    int64_t n, int n_verts, int n_groups, const uint16_t* __restrict__ basis_h3, float t_unscale) {
+    int64_t n, int n_verts, int n_groups, const uint16_t* __restrict__ basis_h3, float t_unscale,
+    int* __restrict__ status) {
   __shared__ f32x4 w_lds[kPairMaxGroups * 64];
   __shared__ PairShared sh;
   for (int i = threadIdx.x; i < n_groups * 64; i += 64 * kPairWaves) {
@@ -681,8 +695,14 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     // Prologue: DMA units 0 .. kAhead - 1 with 3 (dropped) stores after
     // each, so at every step's wait the ops issued after unit k's DMA are
     // the same: kAhead - 1 times (3 stores + a DMA).
-    for (int j = 0; j < kAhead; ++j) {
-      if (j > 0) store(qd, s, 0, false);
+    // (straight-line: no branch between the prologue's DMA groups, so every
+    // control-flow path into the step's wait has the same op sequence --
+    // tools/isa_scan.py checks it on the disassembly)
+    dma(qa, sa, 0);
+    advance(qa, sa);
+#pragma unroll
+    for (int j = 1; j < kAhead; ++j) {
+      store(qd, s, 0, false);
       dma(qa < n_quads ? qa : qd, qa < n_quads ? sa : s, j);
       advance(qa, sa);
     }
@@ -696,14 +716,19 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       for (int j = kPairCompute; j > 0; --j) pend_q[j] = pend_q[j - 1], pend_s[j] = pend_s[j - 1];
       pend_q[0] = qd;
       pend_s[0] = s;
-      if (k >= kPairCompute) {
-        const int ku = k - kPairCompute;
-        if (ok) ok = PAIR_TIMED(pair_wait_ge<MANO_PAIR_SLEEP_MEM>(&sh.done[pair][ku % kPairSlots], ku + 1), stamp);
-        ++stamp.units;
-        PAIR_TIMED_STMT(store(pend_q[kPairCompute], pend_s[kPairCompute], unsigned(ku % kPairSlots), true), t_store);
-      } else {
-        store(qd, s, 0, false);
+      // One store call on every path (its buffer resource drops the bytes
+      // when `real` is false), so the step's vector-memory op sequence has
+      // no branch: 3 stores, then the DMA.
+      const bool drained = k >= kPairCompute;  // unit k - 2 exists
+      const int ku = k - kPairCompute;
+      if (drained && ok) {
+        ok = PAIR_TIMED(pair_wait_ge<MANO_PAIR_SLEEP_MEM>(&sh.done[pair][ku % kPairSlots], ku + 1), stamp);
+        if (!ok) raise_status(status, MANO_DEVICE_SKIN_HANDOFF_TIMEOUT);
       }
+      stamp.units += drained;
+      // after a lost hand-over the stores are issued dropped (same op count)
+      PAIR_TIMED_STMT(store(drained ? pend_q[kPairCompute] : qd, drained ? pend_s[kPairCompute] : s,
+                            drained ? unsigned(ku % kPairSlots) : 0u, drained && ok), t_store);
       // the store's LDS reads have returned (its data is in registers), so
       // unit k - 2's slot is free for unit k + kAhead
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -715,7 +740,10 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     // the last min(k, 2) units
     for (int i = min(k, kPairCompute) - 1; ok && i >= 0; --i) {
       const int ku = k - 1 - i;
-      if (!pair_wait_ge<MANO_PAIR_SLEEP_MEM>(&sh.done[pair][ku % kPairSlots], ku + 1)) break;
+      if (!pair_wait_ge<MANO_PAIR_SLEEP_MEM>(&sh.done[pair][ku % kPairSlots], ku + 1)) {
+        raise_status(status, MANO_DEVICE_SKIN_HANDOFF_TIMEOUT);
+        break;
+      }
       store(pend_q[i], pend_s[i], unsigned(ku % kPairSlots), true);
     }
     // no LDS-DMA may still be writing when the workgroup's LDS is released
@@ -739,7 +767,10 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
   const int cw = (wave - kPairs) / kPairs;
   for (int i = 0; i < cw; ++i) advance(qd, s);
   for (int k = cw; qd < n_quads; k += kPairCompute) {
-    if (!PAIR_TIMED(pair_wait_ge<MANO_PAIR_SLEEP_CMP>(full_flag, k + 1), stamp)) return;
+    if (!PAIR_TIMED(pair_wait_ge<MANO_PAIR_SLEEP_CMP>(full_flag, k + 1), stamp)) {
+      raise_status(status, MANO_DEVICE_SKIN_HANDOFF_TIMEOUT);
+      return;
+    }
     ++stamp.units;
     QuadStage& st = sh.slot[pair][k % kPairSlots];
     if (MANO_QUAD_ABLATE & 2) {  // diagnostic: no compute (the memory waves alone)
@@ -865,7 +896,7 @@ hipError_t launch_skin_quad(const DeviceModel& m, int64_t n, const float* transf
   auto launch = [&](auto kernel) {
     hipLaunchKernelGGL(kernel, dim3(unsigned(blocks)), dim3(64 * kPairWaves), 0, stream, transforms,
                        m.wfrag16, vposed, trans, verts, n, m.n_verts, m.n_groups16, m.basis_h3,
-                       m.h3_lbs_unscale);
+                       m.h3_lbs_unscale, m.status);
   };
   if (h3) {
     if (trans) launch(skin_pair_kernel<true, true>);

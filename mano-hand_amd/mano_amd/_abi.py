@@ -18,6 +18,7 @@ MANO_OK, MANO_EINVAL, MANO_EHIP, MANO_ESMALL, MANO_ESTATE, MANO_ECOMM = 0, -1, -
 MANO_MEMCPY_HOST_TO_DEVICE, MANO_MEMCPY_DEVICE_TO_HOST, MANO_MEMCPY_DEVICE_TO_DEVICE = 1, 2, 3
 MANO_COMM_ID_BYTES = 128
 MANO_PRECISION_FP32, MANO_PRECISION_F16X3 = 0, 1
+MANO_DEVICE_SKIN_HANDOFF_TIMEOUT = 1
 PRECISIONS = {"fp32": MANO_PRECISION_FP32, "f16x3": MANO_PRECISION_F16X3}
 _CODE_NAMES = {MANO_EINVAL: "MANO_EINVAL", MANO_EHIP: "MANO_EHIP",
                MANO_ESMALL: "MANO_ESMALL", MANO_ESTATE: "MANO_ESTATE"}
@@ -31,6 +32,16 @@ class ManoError(RuntimeError):
     def __init__(self, code, message):
         super().__init__(f"{_CODE_NAMES.get(code, code)}: {message}")
         self.code = code
+
+
+class DeviceStatusError(RuntimeError):
+    """A kernel raised a MANO_DEVICE_* bit: some launch's outputs are not valid."""
+
+    def __init__(self, status):
+        names = [n for n, b in (("MANO_DEVICE_SKIN_HANDOFF_TIMEOUT", MANO_DEVICE_SKIN_HANDOFF_TIMEOUT),)
+                 if status & b]
+        super().__init__(f"device status 0x{status:x} ({', '.join(names) or 'unknown bits'})")
+        self.status = status
 
 
 _p = ctypes.c_void_p
@@ -49,6 +60,7 @@ SIGNATURES = {
     "mano_model_set_precision": (ctypes.c_int, [_p, _i32]),
     "mano_model_get_precision": (ctypes.c_int, [_p, ctypes.POINTER(_i32)]),
     "mano_model_info": (ctypes.c_int, [_p, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
+    "mano_model_device_status": (ctypes.c_int, [_p, ctypes.POINTER(_i32), _i32]),
     "mano_workspace_bytes": (ctypes.c_size_t, [_p, _i64]),
     "mano_forward_workspace_bytes": (ctypes.c_size_t, [_p, _i64]),
     "mano_workspace_offsets": (ctypes.c_int, [_p, _i64, ctypes.POINTER(ctypes.c_size_t),

@@ -112,8 +112,11 @@ class AbiGather:
         s = stream if stream is not None else torch.cuda.current_stream(shard.device)
         full = None
         if self.rank == root:
-            full = out if out is not None else torch.empty((n_total,) + tuple(shard.shape[1:]),
-                                                            dtype=shard.dtype, device=shard.device)
+            if out is None:
+                with torch.cuda.stream(s):  # reuse ordered after the recv on `s`
+                    out = torch.empty((n_total,) + tuple(shard.shape[1:]), dtype=shard.dtype,
+                                      device=shard.device)
+            full = out
         _abi.check(_abi.lib().mano_gather(
             self._c, ctypes.c_void_p(shard.data_ptr()), shard.shape[0] * row,
             None if full is None else ctypes.c_void_p(full.data_ptr()), sizes, root,

@@ -97,6 +97,21 @@ class ManoHip:
         self.precision = precision
 
     # ------------------------------------------------------------------ utils
+    def device_status(self, clear: bool = True) -> int:
+        """The model's device status word (include/mano_hip.h
+        mano_model_device_status): 0, or MANO_DEVICE_* bits raised by a launch
+        whose outputs are not valid.  Waits for the device first."""
+        st = ctypes.c_int32()
+        _abi.check(_abi.lib().mano_model_device_status(self._h, ctypes.byref(st), int(clear)))
+        return st.value
+
+    def check_device(self) -> None:
+        """Raise DeviceStatusError if any launch since the last check raised a
+        MANO_DEVICE_* bit (the bits are cleared)."""
+        st = self.device_status(clear=True)
+        if st:
+            raise _abi.DeviceStatusError(st)
+
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
             _abi.check(_abi.lib().mano_model_destroy(self._h))

@@ -17,7 +17,20 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, n), n
         assert n in _abi.SIGNATURES, f"{n} declared in the header but not bound"
     assert set(_abi.SIGNATURES) == set(names)
-    assert lib.mano_abi_version() == 2
+    assert lib.mano_abi_version() == 3
+
+
+@pytest.mark.parametrize("cc,lang", [("g++", "c++"), ("gcc", "c")])
+def test_header_compiles_alone(cc, lang):
+    """include/mano_hip.h is self-contained C and C++ (a stray comment
+    terminator once left prose outside the comment and broke every build)."""
+    import shutil
+    import subprocess
+    if shutil.which(cc) is None:
+        pytest.skip(f"{cc} not installed")
+    r = subprocess.run([cc, "-fsyntax-only", "-Wall", "-Werror", "-x", lang, _abi.HEADER_PATH],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
 
 
 def test_library_is_gfx950_code_object():
@@ -106,3 +119,10 @@ def test_makefile_matches_build_flags():
     assert [os.path.basename(x) for x in srcs] == [os.path.basename(x) for x in g.SRCS]
     extra = {m.group(1): m.group(2).split() for m in re.finditer(r"^\$\(OBJDIR\)/(\S+)\.o: EXTRA := (.*)$", mk, re.M)}
     assert extra == {k: v for k, v in g.SRC_FLAGS.items()}
+
+
+def test_device_status_argument_checks():
+    lib = _abi.lib()
+    st = ctypes.c_int32(7)
+    assert lib.mano_model_device_status(None, ctypes.byref(st), 0) == _abi.MANO_EINVAL
+    assert st.value == 7

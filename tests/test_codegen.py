@@ -43,3 +43,76 @@ def test_no_packed_fp32_valu(report):
 
 def test_no_scalar_stores(report):
     assert report["counts"]["scalar_store"] == 0, report["examples"]["scalar_store"]
+
+
+def test_skin_pair_vmcnt_protocol(report):
+    """skin_pair's memory wave waits with a hand-counted s_waitcnt vmcnt(N):
+    on every control-flow path into that wait the disassembly must end with
+    the awaited unit's DMA group, >= 3 stores, then exactly one DMA group
+    (tools/isa_scan.py), in all four instantiations."""
+    pairs = report["skin_pair_vmcnt"]
+    assert len(pairs) == 4, sorted(pairs)
+    for name, r in pairs.items():
+        assert r["waits"] >= 1 and r["ok"], (name, r)
+
+
+def _tools():
+    import sys
+    p = os.path.join(REPO, "tools")
+    if p not in sys.path:
+        sys.path.insert(0, p)
+    import isa_scan
+    return isa_scan
+
+
+def _prog(ops):
+    """A straight-line instruction list for isa_scan.check_vmcnt_protocol."""
+    code = {"dma": ("buffer_load_dwordx4", "v8, s[0:3], 0 offen lds"),
+            "st": ("buffer_store_dwordx4", "v[0:3], v4, s[0:3], 0 offen"),
+            "wait": ("s_waitcnt", "vmcnt(10)"), "end": ("s_endpgm", "")}
+    return [(4 * i, *code[o], None) for i, o in enumerate(ops)]
+
+
+def test_vmcnt_checker_catches_reordered_ops():
+    """The protocol checker itself: the kernel's order passes; a DMA moved
+    ahead of a store, a missing store or a split group fails."""
+    s = _tools()
+    dma7 = ["dma"] * 7
+    good = dma7 + ["st"] * 3 + dma7 + ["wait", "end"]
+    assert s.check_vmcnt_protocol(_prog(good), 7, 10) == (1, [])
+    bad_order = dma7 + ["st"] * 2 + ["dma", "st"] + ["dma"] * 6 + ["wait", "end"]
+    bad_missing = dma7 + ["st"] * 2 + dma7 + ["wait", "end"]
+    bad_short = dma7 + ["st"] * 3 + ["dma"] * 6 + ["wait", "end"]
+    for prog in (bad_order, bad_missing, bad_short):
+        n, fails = s.check_vmcnt_protocol(_prog(prog), 7, 10)
+        assert n == 1 and fails, prog
+
+
+def test_product_build_sets_no_diagnostic_switch():
+    """Every MANO_* knob the kernel sources read is guarded by csrc/mano_diag.h
+    (#error unless MANO_DIAGNOSTIC_BUILD), and the product build flags
+    (__graft_entry__.py, the Makefile) define none of them."""
+    import re
+    import subprocess
+    import __graft_entry__ as g
+    csrc = os.path.join(REPO, "mano-hand_amd", "csrc")
+    knobs = set()
+    for fn in os.listdir(csrc):
+        knobs |= set(re.findall(r"#ifndef (MANO_[A-Z0-9_]+)", open(os.path.join(csrc, fn)).read()))
+    knobs -= {"MANO_HIP_H"}
+    guard = open(os.path.join(csrc, "mano_diag.h")).read()
+    listed = set(re.findall(r"defined\((MANO_[A-Z0-9_]+)\)", guard)) - {"MANO_DIAGNOSTIC_BUILD"}
+    assert knobs <= listed, sorted(knobs - listed)
+    flags = " ".join(g.FLAGS + [x for v in g.SRC_FLAGS.values() for x in v])
+    mk = open(os.path.join(REPO, "mano-hand_amd", "Makefile")).read()
+    assert "-DMANO" not in flags and "-DMANO" not in mk
+    # the guard fires on a knob and stays quiet without one / in a tools build
+    hdr = os.path.join(csrc, "mano_layout.h")
+    run = lambda *d: subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-x", "c++", *d, hdr],  # noqa: E731
+                                    capture_output=True, text=True)
+    assert run().returncode == 0
+    r = run("-DMANO_BS_ABLATE=1")
+    assert r.returncode != 0 and "diagnostic" in r.stderr
+    assert run("-DMANO_BS_ABLATE=1", "-DMANO_DIAGNOSTIC_BUILD=1").returncode == 0
+    with pytest.raises(ValueError):
+        g.build_library(g.LIB, ["-DMANO_BS_ABLATE=1"])

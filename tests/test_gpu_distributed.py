@@ -80,3 +80,36 @@ def test_dp2_shards_gather_equal_single_process():
     assert verts.shape == (N_TOTAL, 778, 3) and joints.shape == (N_TOTAL, 16, 3)
     assert np.array_equal(verts, ref_v.numpy())
     assert np.array_equal(joints, ref_j.numpy())
+
+
+def test_bench_c4_gather_rehearsal_layout(tmp_path):
+    """bench.py's C4 path with 2 ranks (gloo rehearsal, sharing cuda:0):
+    GPU 0's gathered verts + joints -- the contiguous per-rank layout
+    mano_gather produces -- equal a single-process forward of the global
+    batch bit for bit, and the bench line's own gather_check and
+    correctness leg report it."""
+    import json
+    import subprocess
+    B, world = 300, 2
+    dump = tmp_path / "gather.npz"
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(world), "--backend", "gloo",
+                        "--workload", "C4", "--batch", str(B), "--steps", "3", "--warmup", "1",
+                        "--ramp-seconds", "0", "--no-cpu", "--no-extra", "--no-live-pmc",
+                        "--dump-gather", str(dump)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == world and line["config"]["gather_to_gpu0"]
+    assert line["gather_check"]["bit_exact"] and line["gather_check"]["hands_checked"] > 0
+    assert line["correctness"]["pass"], line["correctness"]
+    with np.load(dump) as z:
+        gv, gj = z["verts"], z["joints"]
+    from mano_amd import ManoHip, synthetic_params
+    m = ManoHip(synthetic_params(0), device=0)
+    inp = m.synthetic_inputs(1003, 0, B * world)   # C4's seed, global indices 0 .. 599
+    out = m.forward(inp["betas"], inp["pose"], None, joints=True)
+    torch.cuda.synchronize()
+    assert gv.shape == (B * world, 778, 3) and gj.shape == (B * world, 16, 3)
+    assert np.array_equal(gv, out["verts"].cpu().numpy())
+    assert np.array_equal(gj, out["joints"].cpu().numpy())
+    m.close()

@@ -9,7 +9,7 @@ set -eu
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 PKG=mano-hand_amd
 SRCS="$PKG/csrc/mano_abi.hip $PKG/csrc/mano_comm.hip $PKG/csrc/mano_pack.cpp $PKG/csrc/mano_articulate.hip $PKG/csrc/mano_kernels.hip $PKG/csrc/mano_kernels_h3.hip $PKG/csrc/mano_skin_quad.hip"
-FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ldl"
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ldl -DMANO_DIAGNOSTIC_BUILD=1"
 if [ "${1:-}" = build ]; then
   /opt/rocm/bin/hipcc $FLAGS -DMANO_H3_NO_PACK=0 -o $PKG/mano_amd/libmano_hip_pack.so $SRCS
   /opt/rocm/bin/hipcc $FLAGS -DMANO_H3_NO_PACK=0 -DMANO_H3_FULL_WAIT=1 -o $PKG/mano_amd/libmano_hip_pack_fullwait.so $SRCS

@@ -1,0 +1,178 @@
+"""Disassembly checks of the built gfx950 library (no HIP runtime needed).
+
+    python tools/isa_scan.py [--json] [path/to/libmano_hip.so]
+
+1. No packed fp32 VALU (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32) in any
+   kernel: the SLP-packed unscale of the f16x3 rest_verts kernels misexecuted
+   (DESIGN.md §4), and packed fp32 is the slower form beside MFMAs.
+2. skin_pair's hand-counted vmcnt protocol (mano_skin_quad.hip, memory
+   wave): the step's `s_waitcnt vmcnt(N)`, N = (kAhead - 1) * (3 + kDmaOps),
+   is correct only if the unit awaited is the DMA group issued 3 + kDmaOps
+   vector-memory ops earlier.  On every control-flow path into each such wait
+   the disassembly must end with: a DMA group (buffer_load ... lds, the awaited
+   unit), at least 3 other vector-memory ops (the stores), then exactly
+   kDmaOps LDS-DMA ops (the next unit), so at least N younger ops cover the
+   awaited group.  A compiler or flag change that reorders or drops one of
+   these ops fails here, on the CPU, instead of racing on the GPU.
+   (`s_cbranch_execz` is taken as not taken: every exec-masked DMA of the
+   memory wave keeps lane 0 active.)
+
+Used by tools/codegen_report.py at build time and by tests/test_gpu_codegen.py
+on the library the GPU tests load (run in a child process started before the
+tests initialise HIP)."""
+import json
+import os
+import re
+import shutil
+import subprocess
+import sys
+import tempfile
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(REPO, "mano-hand_amd", "mano_amd", "libmano_hip.so")
+LLVM = "/opt/rocm/llvm/bin"
+PACKED_FP32 = re.compile(r"\bv_pk_(fma|mul|add)_f32\b")
+# skin_pair memory wave: VMEM ops per LDS-DMA of a unit = 4 rows + 3
+# transform sweeps (+ 1 translation load with kTrans), kAhead = 2.
+SKIN_PAIR = re.compile(r"skin_pair_kernelILb([01])ELb([01])E")
+K_AHEAD, N_STORES, N_ROWS, N_TR = 2, 3, 4, 3
+
+
+def disassemble(lib=LIB):
+    """llvm-objdump -d of every gfx950 code object in the library's fat binary."""
+    work = tempfile.mkdtemp()
+    try:
+        fat = os.path.join(work, "fatbin.bin")
+        subprocess.run([shutil.which("objcopy") or "objcopy", f"--dump-section=.hip_fatbin={fat}", lib],
+                       check=True)
+        data = open(fat, "rb").read()
+        magic = b"__CLANG_OFFLOAD_BUNDLE__"
+        starts = [m.start() for m in re.finditer(re.escape(magic), data)]
+        out = []
+        for k, a in enumerate(starts):
+            b = starts[k + 1] if k + 1 < len(starts) else len(data)
+            part, co = os.path.join(work, f"b{k}.bin"), os.path.join(work, f"b{k}.co")
+            open(part, "wb").write(data[a:b])
+            subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o",
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={part}",
+                            f"--output={co}"], check=True)
+            out.append(subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", "--mcpu=gfx950", co],
+                                      check=True, capture_output=True, text=True).stdout)
+        return "\n".join(out)
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+
+
+_FUNC = re.compile(r"^([0-9a-f]+) <(\S+)>:$")
+_INST = re.compile(r"^\s+(\S+)(.*?)\s*//\s*([0-9A-Fa-f]+):")
+_TARGET = re.compile(r"<(\S+)\+0x([0-9a-f]+)>\s*$")
+
+
+def functions(asm):
+    """{name: [(addr, mnemonic, operands, target_addr or None)]} per function."""
+    funcs, cur, base = {}, None, 0
+    for line in asm.splitlines():
+        m = _FUNC.match(line)
+        if m:
+            base, cur = int(m.group(1), 16), m.group(2)
+            funcs[cur] = []
+            continue
+        if cur is None:
+            continue
+        m = _INST.match(line)
+        if not m:
+            continue
+        tgt = None
+        t = _TARGET.search(line)
+        if t and m.group(1).startswith(("s_branch", "s_cbranch")):
+            tgt = base + int(t.group(2), 16) if t.group(1) == cur else None
+        funcs[cur].append((int(m.group(3), 16), m.group(1), m.group(2).strip(), tgt))
+    return funcs
+
+
+def _vmem_kind(mn, ops):
+    """'dma' (LDS-DMA), 'vmem' (other vector-memory op) or None."""
+    if mn.startswith(("buffer_", "global_", "flat_", "scratch_")):
+        if mn.startswith(("buffer_load", "global_load")) and re.search(r"\blds\b", ops):
+            return "dma"
+        if mn.startswith(("buffer_wbl2", "buffer_inv")):
+            return None
+        return "vmem"
+    return None
+
+
+def check_vmcnt_protocol(insts, n_dma, n_wait):
+    """Every path from the function entry to each `s_waitcnt vmcnt(n_wait)`
+    must end with [dma]+ [other]{>=3} [dma]{n_dma} (see the module docstring).
+    Returns (n_waits_found, [failure strings])."""
+    idx = {a: i for i, (a, _, _, _) in enumerate(insts)}
+    waits = {i for i, (_, mn, ops, _) in enumerate(insts)
+             if mn == "s_waitcnt" and re.search(rf"\bvmcnt\({n_wait}\)", ops)}
+    keep = n_dma + 3 + 8
+    failures, seen, stack = [], set(), [(0, ())]
+    while stack:
+        i, tail = stack.pop()
+        while i < len(insts):
+            state = (i, tail)
+            if state in seen:
+                break
+            seen.add(state)
+            a, mn, ops, tgt = insts[i]
+            if i in waits:
+                k = len(tail)
+                last = tail[k - n_dma:] if k >= n_dma else ()
+                j = k - n_dma
+                n_other = 0
+                while j - 1 >= 0 and tail[j - 1] != "dma":
+                    n_other += 1
+                    j -= 1
+                ok = (len(last) == n_dma and all(x == "dma" for x in last)
+                      and (k - n_dma - 1 < 0 or tail[k - n_dma - 1] != "dma")
+                      and n_other >= N_STORES and j - 1 >= 0 and tail[j - 1] == "dma")
+                if not ok:
+                    failures.append(f"wait at 0x{a:x}: ops before it {list(tail)}")
+            kind = _vmem_kind(mn, ops)
+            if kind:
+                tail = (tail + (kind,))[-keep:]
+            if mn == "s_endpgm":
+                break
+            if mn == "s_branch":
+                if tgt is None or tgt not in idx:
+                    failures.append(f"unresolved branch at 0x{a:x}")
+                    break
+                i = idx[tgt]
+                continue
+            if mn.startswith("s_cbranch") and mn != "s_cbranch_execz":
+                if tgt is None or tgt not in idx:
+                    failures.append(f"unresolved branch at 0x{a:x}")
+                    break
+                stack.append((idx[tgt], tail))
+            i += 1
+    return len(waits), failures
+
+
+def scan(lib=LIB):
+    asm = disassemble(lib)
+    funcs = functions(asm)
+    pairs = {}
+    for name, insts in funcs.items():
+        m = SKIN_PAIR.search(name)
+        if not m:
+            continue
+        trans = m.group(1) == "1"
+        n_dma = N_ROWS + N_TR + (1 if trans else 0)
+        n_wait = (K_AHEAD - 1) * (N_STORES + n_dma)
+        n_found, fails = check_vmcnt_protocol(insts, n_dma, n_wait)
+        pairs[name] = {"trans": trans, "h3": m.group(2) == "1", "dma_ops": n_dma, "vmcnt": n_wait,
+                       "waits": n_found, "failures": fails[:5], "ok": n_found > 0 and not fails}
+    packed = [l.strip() for l in asm.splitlines() if PACKED_FP32.search(l)]
+    return asm, {"packed_fp32": len(packed), "packed_fp32_examples": packed[:5],
+                 "skin_pair_vmcnt": pairs,
+                 "mfma": {op: len(re.findall(rf"\b{op}\b", asm))
+                          for op in sorted(set(re.findall(r"\bv_mfma_\w+", asm)))}}
+
+
+if __name__ == "__main__":
+    args = [a for a in sys.argv[1:] if a != "--json"]
+    _, rep = scan(*args)
+    print(json.dumps(rep) if "--json" in sys.argv else json.dumps(rep, indent=1))
