@@ -19,6 +19,7 @@
 #include <algorithm>
 
 #include "mano_internal.h"
+#include "mano_joint.h"
 #include "mano_span.h"
 
 namespace mano {
@@ -345,12 +346,38 @@ __device__ __forceinline__ void bs_stamp(int slot, unsigned long long v) {
 #ifndef MANO_BS_BLOCKS_PER_CU
 #define MANO_BS_BLOCKS_PER_CU 3  // resident blocks per CU (diagnostic builds: 1, 2, 4)
 #endif
-template <bool kTrans, bool kVposed>
+// The single-launch forward (kArt): blend_skin16 articulates each hand tile
+// itself at the start of every range of its units -- articulate_kernel's lane
+// per (hand, joint), 4 rounds of 4 hands per wave (mano_joint.h), the X rows
+// and transforms written to the workspace exactly as articulate_kernel writes
+// them and read straight back by the same wave (L2), posed joints written by
+// the block that owns the tile set's first vertex group.  The articulation's
+// HBM writes (1.4 KB per hand) then drain behind the MFMA work instead of
+// forming a launch of their own.
+struct ArtArgs {
+  const float* betas;
+  int64_t betas_stride;
+  const float* pose;
+  const float* joint_template;  // [16][3]
+  const float* joint_shape;     // [16][3][10]
+  const int32_t* parents;
+  const int32_t* depth;
+  int max_depth;
+  float* joints;                // nullable: posed joints (+ trans)
+  float* features;              // workspace X rows (written, then read back)
+  float* transforms;            // workspace transforms (written, then read back)
+};
+
+template <bool kTrans, bool kVposed, bool kArt = false>
 __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kernel(
-    const float* __restrict__ features, const float* __restrict__ transforms,
+    const float* __restrict__ features_in, const float* __restrict__ transforms_in,
     const float* __restrict__ basis16, const float* __restrict__ wfrag16,
     const float* __restrict__ trans, float* __restrict__ verts, float* __restrict__ vposed,
-    int64_t n, int n_verts, int n_groups) {
+    int64_t n, int n_verts, int n_groups, ArtArgs art) {
+  // kArt: the X rows / transforms are this kernel's own output, so they are
+  // read through plain (aliasing) pointers, never as const __restrict__.
+  const float* features = kArt ? art.features : features_in;
+  const float* transforms = kArt ? art.transforms : transforms_in;
   // One slot: a basis tile (10 KB) + the group's W fragment (1 KB, with the
   // group's first tile); ring of 3.
   constexpr int kRingF4 = (kGroups16 + 1) * 64;
@@ -361,14 +388,31 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
   // group's first tile, the previous group's stores.
   constexpr int kPieces = kGroups16 / 4;     // LDS-DMA pieces per wave and tile, at least
   constexpr int kDmaPrio = MANO_BS_DMA_PRIO, kStorePrio = MANO_BS_STORE_PRIO;
-  __shared__ f32x4 lds[kSlots * kRingF4];
+  constexpr int kJtJs = kJoints * 3 + kJoints * 3 * kShape;  // folded joint regressor, 528 floats
+  // kArt: the folded regressor sits behind the ring in the same array (a
+  // second LDS array made hipcc wait vmcnt(0) for the ring's DMA before
+  // every LDS read of the group loop)
+  __shared__ f32x4 lds[kSlots * kRingF4 + (kArt ? kJtJs / 4 : 0)];
   __shared__ float trs[4][16 * 3];  // the wave's 16 translations, read back at the stores
+  float* const jreg_s = reinterpret_cast<float*>(lds + kSlots * kRingF4);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int vstride32 = 3 * n_verts;
   const int64_t nt16 = (n + 15) / 16;
   const int64_t n_quads = (nt16 + 3) / 4;
   int64_t u, u_end;
   unit_range(n_quads * n_groups, blockIdx.x, gridDim.x, u, u_end);
+  int art_src = 0, art_dep = 0;
+  if constexpr (kArt) {
+    // once per block: the folded regressor (J = Jt + Js . beta) into LDS and
+    // this lane's joint's parent lane and tree depth (lane & 15 = joint)
+    for (int i = threadIdx.x; i < kJtJs; i += 256)
+      jreg_s[i] = i < kJoints * 3 ? art.joint_template[i] : art.joint_shape[i - kJoints * 3];
+    const int j = threadIdx.x & 15;
+    const int par = art.parents[j];
+    art_src = ((threadIdx.x & 63) & ~15) + (par < 0 ? 0 : par);
+    art_dep = art.depth[j];
+    __syncthreads();
+  }
 #if MANO_BS_STAMP
   bs_stamp(0, __builtin_amdgcn_s_memtime());
   bs_stamp(2, __builtin_amdgcn_s_memrealtime());
@@ -400,6 +444,50 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
     asm volatile("" : "+v"(lane));
     const int row0 = 4 * (lane >> 4);  // D rows (hands) of this lane: row0 + r
     const int col = lane & 15;         // D column (vertex of the group)
+
+    if constexpr (kArt) {
+      // Articulate the wave's 16 hands: round r takes hands 4r .. 4r + 3, a
+      // lane per (hand, joint), exactly articulate_kernel's arithmetic and
+      // output layout (rows past the batch end repeat the last hand, as the
+      // A-fragment loads below do, so every store is of identical values).
+      const int j = lane & 15;
+      const bool own_joints = art.joints != nullptr && g0 == 0;  // one block per tile set
+#pragma unroll 1
+      for (int r = 0; r < 4; ++r) {
+        const int64_t hh = h0 + 4 * r + (lane >> 4);
+        const int64_t h = hh < n ? hh : n - 1;
+        const float* pp = art.pose + h * (kJoints * 3) + 3 * j;
+        const float ax = pp[0], ay = pp[1], az = pp[2];
+        float beta[kShape];
+#pragma unroll
+        for (int k = 0; k < kShape; ++k) beta[k] = art.betas[h * art.betas_stride + k];
+        float rm[9], J[3], t[3], Aj[12];
+        articulate_joint(ax, ay, az, beta, j, art_src, art_dep, art.max_depth, jreg_s,
+                         jreg_s + kJoints * 3, rm, J, t, Aj);
+        f32x4* A = reinterpret_cast<f32x4*>(art.transforms + h * kTransformFloats + j * 12);
+        A[0] = f32x4{Aj[0], Aj[1], Aj[2], Aj[3]};
+        A[1] = f32x4{Aj[4], Aj[5], Aj[6], Aj[7]};
+        A[2] = f32x4{Aj[8], Aj[9], Aj[10], Aj[11]};
+        float* x = art.features + h * kXStride;
+        if (j == 0) {
+#pragma unroll
+          for (int k = 0; k < kShape; ++k) x[x_pos(k)] = beta[k];
+          x[x_pos(kK)] = 1.f;
+#pragma unroll
+          for (int k = kK + 1; k < kXStride; ++k) x[x_pos(k)] = 0.f;
+        } else {
+#pragma unroll
+          for (int m = 0; m < 9; ++m) x[x_pos(kShape + 9 * (j - 1) + m)] = rm[m];
+        }
+        if (own_joints && hh < n) {
+          float* o = art.joints + hh * (kJoints * 3) + 3 * j;
+#pragma unroll
+          for (int c = 0; c < 3; ++c) o[c] = t[c] + (kTrans ? trans[hh * 3 + c] : 0.f);
+        }
+      }
+      // the rows and transforms are in L2 before this wave reads them back
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
 
     float a[kGroups16 * 4];
     float F[12][4];  // LBS A fragments, tile (c, k) = c * 4 + k, resident for the quad
@@ -519,6 +607,151 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
   bs_stamp(6, (unsigned long long)n_ranges);
   bs_stamp(7, t_first | (t_prologue << 32));
 #endif
+}
+
+// ---------------------------------------------------------------------------
+// blend_skin16w: blend_skin16's arithmetic with one 12-wave block per CU
+// (3 waves per SIMD, each its own 16-hand tile, so a unit is a set of 12
+// tiles x one vertex group) sharing ONE basis ring of two group slots: the
+// block stages each group's 3 basis tiles + W fragment once for 192 hands
+// (blend_skin16: once per 64 hands, three rings per CU), every wave issues
+// exactly 3 LDS-DMA pieces per group (31 real pieces, the rest land in a
+// sink), and there is one barrier per group instead of three: group g + 1
+// is staged while group g is computed, and the barrier after g's stores
+// waits for that DMA (counted vmcnt: the stores stay in flight) and for
+// every wave to leave g's slot before g + 2 overwrites it.  Same MFMA chains
+// and apply order as blend_skin16: identical bits.
+// ---------------------------------------------------------------------------
+#ifndef MANO_BS_WIDE
+#define MANO_BS_WIDE 0
+#endif
+constexpr int kWideWaves = 12;
+constexpr int kWideGroupF4 = (3 * kGroups16 + 1) * 64;   // 3 tiles + W: 31 KB
+constexpr int kWidePieces = 3;                            // DMA ops per wave and group
+static_assert(kWideWaves * kWidePieces >= 3 * kGroups16 + 1, "pieces per group");
+
+template <bool kTrans, bool kVposed>
+__global__ __launch_bounds__(64 * kWideWaves, 3) void blend_skin16w_kernel(
+    const float* __restrict__ features, const float* __restrict__ transforms,
+    const float* __restrict__ basis16, const float* __restrict__ wfrag16,
+    const float* __restrict__ trans, float* __restrict__ verts, float* __restrict__ vposed,
+    int64_t n, int n_verts, int n_groups) {
+  constexpr int kStores = kVposed ? 8 : 4;  // global_store_dwordx3 per group
+  __shared__ f32x4 lds[2 * kWideGroupF4];
+  __shared__ f32x4 sink[64];                 // the padding pieces land here
+  __shared__ float trs[kWideWaves][16 * 3];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int vstride32 = 3 * n_verts;
+  const int64_t nt16 = (n + 15) / 16;
+  const int64_t n_sets = (nt16 + kWideWaves - 1) / kWideWaves;
+  int64_t u, u_end;
+  unit_range(n_sets * n_groups, blockIdx.x, gridDim.x, u, u_end);
+
+  // Piece p = 3 wave + i of group grp: p < 30 basis tile p / 10, K-group
+  // p % 10; p == 30 the W fragment; p > 30 the sink (a valid 1-KB read).
+  auto stage_group = [&](int grp, f32x4* slot, int lane) {
+    unsigned lane_off = unsigned(lane) * 16u;
+    asm volatile("" : "+v"(lane_off));
+    const char* bsrc = reinterpret_cast<const char*>(basis16 + int64_t(3 * grp) * kTile16Floats);
+    const char* wsrc = reinterpret_cast<const char*>(wfrag16 + int64_t(grp) * kWFrag16Floats);
+#pragma unroll
+    for (int i = 0; i < kWidePieces; ++i) {
+      const int p = kWidePieces * wave + i;
+      const char* src;
+      f32x4* dst;
+      if (p < 3 * kGroups16) {
+        src = bsrc + unsigned(p) * 1024u;   // tile p / 10, K-group p % 10: contiguous 1-KB pieces
+        dst = slot + p * 64;
+      } else if (p == 3 * kGroups16) {
+        src = wsrc;
+        dst = slot + 3 * kGroups16 * 64;
+      } else {
+        src = wsrc;
+        dst = sink;
+      }
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + lane_off),
+                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+
+  while (u < u_end) {
+    const int64_t set = u / n_groups;
+    const int g0 = int(u - set * n_groups);
+    const int g1 = int(n_groups - g0 < u_end - u ? n_groups : g0 + (u_end - u));
+    u += g1 - g0;
+    const int64_t h0 = min(set * kWideWaves + wave, nt16 - 1) * 16;
+    const int n_valid = int(n - h0 < 16 ? n - h0 : 16);
+    int lane = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane));
+    const int row0 = 4 * (lane >> 4);
+    const int col = lane & 15;
+
+    float a[kGroups16 * 4];
+    float F[12][4];
+    const int64_t row = min(h0 + (lane & 15), n - 1);
+    const f32x4* src = reinterpret_cast<const f32x4*>(features + row * kXStride) + (lane >> 4);
+#pragma unroll
+    for (int g = 0; g < kGroups16; ++g) {
+      const f32x4 v = src[4 * g];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[4 * g + q] = v[q];
+    }
+    load_lbs_frags(transforms, h0, n, lane, F);
+    if constexpr (kTrans) {
+      if (lane < 48) {
+        const int64_t h = h0 + lane / 3;
+        trs[wave][lane] = trans[(h < n ? h : n - 1) * 3 + lane % 3];
+      }
+    }
+    float* vtile = verts + h0 * int64_t(vstride32);
+    float* ptile = kVposed ? vposed + h0 * int64_t(vstride32) : nullptr;
+
+    stage_group(g0, lds, lane);
+    barrier_vmcnt<0>();  // group g0's slot and every prologue load have landed
+
+    for (int grp = g0; grp < g1; ++grp) {
+      int glane = threadIdx.x & 63;  // opaque per group: no lane address kept live across the loop
+      asm volatile("" : "+v"(glane));
+      f32x4* slot = lds + ((grp - g0) & 1) * kWideGroupF4;
+      // read before the next group's DMA is issued (hipcc cannot tell the
+      // slots apart and would wait for the DMA before a later read)
+      const f32x4 wf = slot[3 * kGroups16 * 64 + glane];
+      prio_up<MANO_BS_DMA_PRIO>();
+      if (grp + 1 < g1) stage_group(grp + 1, lds + ((grp + 1 - g0) & 1) * kWideGroupF4, glane);
+      prio_down<MANO_BS_DMA_PRIO>();
+      __builtin_amdgcn_sched_barrier(0);
+      f32x4 p[3];
+      p[0] = mfma16_tile(a, slot, glane);
+      __builtin_amdgcn_sched_barrier(0);
+      p[1] = mfma16_tile(a, slot + kGroups16 * 64, glane);
+      __builtin_amdgcn_sched_barrier(0);
+      p[2] = mfma16_tile(a, slot + 2 * kGroups16 * 64, glane);
+      __builtin_amdgcn_sched_barrier(0);
+      int vb = grp * 16;
+      if (vb > n_verts - 16) vb = n_verts - 16;
+      const int voff = 3 * (vb + col);
+      f32x4 out[3];
+      lbs_apply16(F, wf, p, out);
+      __builtin_amdgcn_sched_barrier(0);  // store addresses computed here, not across the chains
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int hr = min(row0 + r, n_valid - 1);
+        float o0 = out[0][r], o1 = out[1][r], o2 = out[2][r];
+        if constexpr (kTrans) {
+          o0 += trs[wave][hr * 3 + 0];
+          o1 += trs[wave][hr * 3 + 1];
+          o2 += trs[wave][hr * 3 + 2];
+        }
+        store_out<MANO_BS_NT_STORE && !kVposed>(vtile + unsigned(hr * vstride32 + voff), f32x3{o0, o1, o2});
+        if constexpr (kVposed)
+          store_out<false>(ptile + unsigned(hr * vstride32 + voff), f32x3{p[0][r], p[1][r], p[2][r]});
+      }
+      // group grp + 1's pieces have landed (only the stores are younger) and
+      // no wave still reads grp's slot, which grp + 2 is staged into next
+      if (grp + 1 < g1) barrier_vmcnt<kStores>();
+    }
+    barrier_vmcnt<kStores>();  // the range's last slot is free for the next range's prologue
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -717,12 +950,49 @@ hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* featu
   auto launch = [&](auto kernel) {
     hipLaunchKernelGGL(kernel, persistent_grid(kernel, m, n_quads * m.n_groups16, 1, kBlendSkinBlocksPerCU),
                        dim3(256), 0, stream, features, transforms, m.basis16, m.wfrag16, trans, verts,
-                       vposed, n, m.n_verts, m.n_groups16);
+                       vposed, n, m.n_verts, m.n_groups16, ArtArgs{});
   };
+#if MANO_BS_WIDE
+  const int64_t n_sets = ((n + 15) / 16 + kWideWaves - 1) / kWideWaves;
+  auto launch_w = [&](auto kernel) {
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, 64 * kWideWaves, 0) != hipSuccess || b < 1) b = 1;
+    const int64_t cap = int64_t(1) * (m.n_cu > 0 ? m.n_cu : 1);
+    const int64_t want = (n_sets * m.n_groups16 + kMinUnitsPerWorker - 1) / kMinUnitsPerWorker;
+    hipLaunchKernelGGL(kernel, dim3(unsigned(want < cap ? want : cap)), dim3(64 * kWideWaves), 0, stream,
+                       features, transforms, m.basis16, m.wfrag16, trans, verts, vposed, n, m.n_verts,
+                       m.n_groups16);
+  };
+  if (trans && vposed) launch_w(blend_skin16w_kernel<true, true>);
+  else if (trans) launch_w(blend_skin16w_kernel<true, false>);
+  else if (vposed) launch_w(blend_skin16w_kernel<false, true>);
+  else launch_w(blend_skin16w_kernel<false, false>);
+  return hipGetLastError();
+#endif
   if (trans && vposed) launch(blend_skin16_kernel<true, true>);
   else if (trans) launch(blend_skin16_kernel<true, false>);
   else if (vposed) launch(blend_skin16_kernel<false, true>);
   else launch(blend_skin16_kernel<false, false>);
+  return hipGetLastError();
+}
+
+// The single-launch forward: blend_skin16 with the articulation in its range
+// prologue (kArt).  The workspace's X rows and transforms are written and read
+// by the kernel itself.
+hipError_t launch_forward_fused(const DeviceModel& m, int64_t n, const float* betas,
+                                int64_t betas_stride, const float* pose, const float* trans,
+                                float* verts, float* joints, float* features, float* transforms,
+                                hipStream_t stream) {
+  const int64_t n_quads = ((n + 15) / 16 + 3) / 4;
+  const ArtArgs art{betas, betas_stride, pose, m.joint_template, m.joint_shape, m.parents, m.depth,
+                    m.max_depth, joints, features, transforms};
+  auto launch = [&](auto kernel) {
+    hipLaunchKernelGGL(kernel, persistent_grid(kernel, m, n_quads * m.n_groups16, 1, kBlendSkinBlocksPerCU),
+                       dim3(256), 0, stream, nullptr, nullptr, m.basis16, m.wfrag16, trans, verts, nullptr,
+                       n, m.n_verts, m.n_groups16, art);
+  };
+  if (trans) launch(blend_skin16_kernel<true, false, true>);
+  else launch(blend_skin16_kernel<false, false, true>);
   return hipGetLastError();
 }
 

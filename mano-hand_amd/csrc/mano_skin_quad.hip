@@ -442,6 +442,14 @@ constexpr int kPairCompute = MANO_QUAD_PAIR_COMPUTE;
 constexpr int kPairSlots = MANO_PAIR_SLOTS;
 
 constexpr int kPairWaves = kPairs * (1 + kPairCompute);
+// Hand quads in reverse order: the unfused path's blend GEMM writes v_posed
+// in hand order, so its last ~256 MB are still dirty in the Infinity Cache
+// when the LBS starts; taken last-first, those rows are read (and their
+// lines retired) before the stream pushes them out to HBM.
+#ifndef MANO_PAIR_REVERSE
+#define MANO_PAIR_REVERSE 0
+#endif
+constexpr bool kPairReverse = MANO_PAIR_REVERSE;
 constexpr int kPairMaxGroups = 52;  // W in LDS beside the slots: V <= 832
 
 struct PairShared {
@@ -642,7 +650,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     constexpr int kTrOps = (MANO_QUAD_ABLATE & 4) ? 0 : kQTrF4;
     constexpr int kDmaOps = kQHands + kTrOps + (kTrans ? 1 : 0);
     auto dma = [&](int64_t fq, int fs, int slot) {
-      const int64_t h0 = fq * kQHands;
+      const int64_t h0 = (kPairReverse ? n_quads - 1 - fq : fq) * kQHands;
       const int valid = int(n - h0 < kQHands ? n - h0 : kQHands);
       const auto rv = rsrc(vposed + h0 * vstride, int64_t(valid) * vstride);
       const auto rt = rsrc(transforms + h0 * kTransformFloats, int64_t(valid) * kTransformFloats);
@@ -670,7 +678,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     constexpr unsigned kSlotBytes = sizeof(QuadStage);
     auto store = [&](int64_t fq, int fs, unsigned slot, bool real) {
       const unsigned so = slot * kSlotBytes;
-      const int64_t h0 = fq * kQHands;
+      const int64_t h0 = (kPairReverse ? n_quads - 1 - fq : fq) * kQHands;
       const int valid = real ? int(n - h0 < kQHands ? n - h0 : kQHands) : 0;  // 0: every store dropped
       const auto ro = rsrc(verts + h0 * vstride, int64_t(valid) * vstride);
       const bool full = fs < n_full;
