@@ -2,11 +2,9 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload C2|C3|C4|C5]
 
-One step = one forward pass (mano_forward for verts + joints: ONE launch of the
-fused kernel that articulates each hand tile, runs the blend GEMM and the LBS)
-over the workload's hands per GPU, inputs resident in HBM before the timed
-region.  `--path staged` times the round-2 step (articulate, then the fused
-blend GEMM + LBS), `--path unfused` the three-kernel form.  Workloads (BASELINE.json configs; per-GPU shard
+One step = one forward pass (mano_forward: articulate, then the fused blend
+GEMM + LBS kernel) over the workload's hands per GPU, inputs resident in HBM
+before the timed region.  Workloads (BASELINE.json configs; per-GPU shard
 fixed as N grows, so `scaling` is "weak"):
 
   C2  65,536 hands per GPU, full pose + per-hand betas, verts + joints (default:
@@ -89,10 +87,9 @@ def parse(argv=None):
     ap.add_argument("--event-every", type=int, default=8,
                     help="bracket the kernels of every E-th timed step with HIP events (1 = every step; "
                          "each timing event costs the step ~4 us, tools/debug/time_events.py)")
-    ap.add_argument("--path", choices=("forward", "staged", "unfused"), default="forward",
-                    help="forward: one mano_forward call per step = ONE launch, the fused kernel that "
-                         "articulates, blends and skins (default); staged: articulate + blend_skin16 as "
-                         "two stage launches; unfused: articulate + blend + skin")
+    ap.add_argument("--path", choices=("forward", "api", "unfused"), default="forward",
+                    help="forward: mano_forward's two kernels, each bracketed by events (default); "
+                         "api: one mano_forward call per step; unfused: articulate + blend + skin")
     ap.add_argument("--precision", choices=("fp32", "f16x3"), default="fp32",
                     help="fp32: exact fp32 MFMA (default); f16x3: split-half MFMA "
                          "(include/mano_hip.h MANO_PRECISION_F16X3)")
@@ -203,6 +200,22 @@ def check_sample(model, seed, first, B, betas, pose, trans, verts, joints, model
     return res
 
 
+def merge_checks(per_rank):
+    """Rank 0's summary of every rank's check_sample result: the max errors
+    over all shards, pass only if every rank passed."""
+    ok = [r for r in per_rank if r and "max_abs_err_verts" in r]
+    if len(ok) != len(per_rank):
+        return {"error": "a rank's correctness leg failed", "per_rank": per_rank}
+    out = dict(max(ok, key=lambda r: r["max_abs_err_verts"]))
+    out["max_abs_err_joints"] = max(r["max_abs_err_joints"] for r in ok)
+    out["n_sampled"] = sum(r["n_sampled"] for r in ok)
+    out["ranks_checked"] = len(ok)
+    out["pass"] = all(r["pass"] for r in ok)
+    out["finite"] = all(r["finite"] for r in ok)
+    out["device_status"] = max(r.get("device_status", 0) for r in ok)
+    return out
+
+
 def check_gather(model, seed, B, world, gv, gj, with_trans, per_rank=64):
     """GPU 0's gathered buffers vs a local forward: from every rank's range
     [r B, (r + 1) B) the first 16, last 16 and a random run of 32 hands are
@@ -259,8 +272,7 @@ def load_traffic(path, kernel, batch):
 
 # Demangled-name fragment of each dominant kernel (rocprofv3 Kernel_Name).
 PMC_KERNEL_NAME = {"blend_skin": "::blend_skin16_kernel<", "blend_skin_h3": "::blend_skin_h3_kernel<",
-                   "blend": "::blend_kernel(", "skin": "::skin_pair_kernel<", "forward": "::blend_skin16_kernel<",
-                   "forward_h3": "::blend_skin_h3_kernel<"}
+                   "blend": "::blend_kernel(", "skin": "::skin_pair_kernel<", "mano_forward": "::blend_skin16_kernel<"}
 
 
 def pmc_values(d, counter, name_fragment):
@@ -395,24 +407,23 @@ def main(argv=None):
             gj = torch.empty((B * world, 16, 3), device=dev)
 
     # Launch sequence of one step; `marks` get an event after each kernel.
-    # "forward" is exactly what mano_forward issues for verts + joints: one
-    # launch (blend_skin16 articulating its own hand tiles); "staged" the
-    # round-2 step (articulate, then the fused blend GEMM + LBS); "unfused"
-    # articulate, blend GEMM (v_posed to HBM), LBS.
+    # "forward" issues exactly mano_forward's two launches (articulate, then
+    # the fused blend GEMM + LBS) through the stage calls so that each kernel
+    # is bracketed by events on its stream; "api" is one mano_forward call.
     def run_path(path, marks=None):
         def mark(i):
             if marks is not None:
                 marks[i].record(stream)
         mark(0)
         if path == "forward":
-            model.forward(betas, pose, trans, joints=True, out=out)
-            mark(1)
-        elif path == "staged":
             model.stage_articulate(betas, pose, trans, joints=joints)
             mark(1)
             model.stage_blend_skin(B, verts, trans=trans)
             mark(2)
-        else:  # unfused
+        elif path == "api":
+            model.forward(betas, pose, trans, joints=True, out=out)
+            mark(1)
+        else:  # unfused: articulate, blend GEMM (v_posed to HBM), LBS
             model.stage_articulate(betas, pose, trans, joints=joints)
             mark(1)
             model.stage_blend(B)
@@ -420,7 +431,7 @@ def main(argv=None):
             model.stage_skin(B, verts, trans=trans)
             mark(3)
 
-    n_marks = {"forward": 2, "staged": 3, "unfused": 4}
+    n_marks = {"forward": 3, "api": 2, "unfused": 4}
 
     def step(marks=None):
         run_path(args.path, marks)
@@ -479,8 +490,8 @@ def main(argv=None):
     # Per-kernel table.  The timed path's kernels come from the timed steps;
     # the other paths' kernels are timed on the same stream afterwards (rank 0,
     # not part of `value`), so every kernel's roofline is reported each run.
-    timed = {"forward": {"forward": (0, 1)},
-             "staged": {"articulate": (0, 1), "blend_skin": (1, 2)},
+    timed = {"forward": {"articulate": (0, 1), "blend_skin": (1, 2)},
+             "api": {"mano_forward": (0, 1)},
              "unfused": {"articulate": (0, 1), "blend": (1, 2), "skin": (2, 3)}}
     sampled = [e for e in events if e is not None]
     ms = {k: span(a, b, sampled) for k, (a, b) in timed[args.path].items()}
@@ -497,7 +508,7 @@ def main(argv=None):
             torch.cuda.synchronize()
             for k, (a, b) in timed[path].items():
                 into.setdefault(k, span(a, b, evs))
-        for path in ("forward", "staged", "unfused"):
+        for path in ("forward", "api", "unfused"):
             if path != args.path:
                 time_path(path, ms)
         # The standalone LBS back to back (each launch after another LBS
@@ -513,7 +524,7 @@ def main(argv=None):
         torch.cuda.synchronize()
         ms["skin_back_to_back"] = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
         model.set_precision(other)
-        for path in ("staged", "unfused"):
+        for path in ("forward", "unfused"):
             time_path(path, ms_other)
         model.set_precision(args.precision)
 
@@ -523,23 +534,12 @@ def main(argv=None):
     def gbs(nbytes, t):
         return nbytes * B / (t * 1e-3) / 1e9
 
-    in_path = {"forward": ("forward",), "staged": ("articulate", "blend_skin"),
+    in_path = {"forward": ("articulate", "blend_skin"), "api": ("mano_forward",),
                "unfused": ("articulate", "blend", "skin")}[args.path]
     kernels = {}
-    if "forward" in ms and args.precision == "fp32":
-        a = tflops(FUSED_MFMA_FLOP_PER_HAND, ms["forward"])
-        kernels["forward"] = {"kernel": "blend_skin16_kernel<kArt> (mano_forward: articulation + blend GEMM + "
-                                        "LBS in one launch)",
-                              "ms": ms["forward"], "bound": "mfma", "achieved_TFLOPs": a,
-                              "frac": a / PEAK_FP32_TFLOPS, "flop_per_hand": FUSED_MFMA_FLOP_PER_HAND,
-                              "flop_per_hand_note": "MFMA work only (blend GEMM + LBS transform blend); "
-                                                    "the articulation's ~3,300 VALU flop/hand not counted"}
-    elif "forward" in ms:  # f16x3: mano_forward is articulate + blend_skin_h3
-        kernels["forward"] = {"kernel": "articulate_kernel + blend_skin_h3_kernel (mano_forward)",
-                              "ms": ms["forward"], "bound": "hbm",
-                              "achieved_GBs": gbs(FUSED_BYTES_PER_HAND + ARTICULATE_BYTES_PER_HAND, ms["forward"]),
-                              "frac": gbs(FUSED_BYTES_PER_HAND + ARTICULATE_BYTES_PER_HAND, ms["forward"]) / PEAK_HBM_GBS,
-                              "bytes_per_hand": FUSED_BYTES_PER_HAND + ARTICULATE_BYTES_PER_HAND}
+    if "mano_forward" in ms:
+        kernels["mano_forward"] = {"kernel": "articulate_kernel + blend_skin16_kernel (one ABI call)",
+                                   "ms": ms["mano_forward"]}
     if "articulate" in ms:
         a = gbs(ARTICULATE_BYTES_PER_HAND, ms["articulate"])
         kernels["articulate"] = {"kernel": "articulate_kernel", "ms": ms["articulate"],
@@ -577,7 +577,7 @@ def main(argv=None):
         v["in_timed_path"] = k in in_path
         v["precision"] = args.precision
     # The other precision mode's kernels (timed after the timed region, not in `value`).
-    if "blend_skin" in ms_other and "articulate" in ms_other:
+    if "blend_skin" in ms_other:
         t = ms_other["blend_skin"]
         kernels[f"blend_skin_{other}"] = {
             "kernel": "blend_skin_h3_kernel" if other == "f16x3" else "blend_skin16_kernel",
@@ -597,8 +597,8 @@ def main(argv=None):
     # Roofline of the dominant kernel of the timed path.
     if args.path == "unfused":
         dominant = "blend" if ms["blend"] >= ms["skin"] else "skin"
-    elif args.path == "forward":
-        dominant = "forward"
+    elif args.path == "api":
+        dominant = "blend_skin" if "blend_skin" in kernels else None
     else:
         dominant = "blend_skin"
     roof = None
@@ -631,14 +631,27 @@ def main(argv=None):
         roof["timed_in_region"] = dominant in in_path
 
     # Correctness of the timed outputs (the last timed step's verts / joints):
-    # sampled hands vs the float64 oracle in a child process, and at N > 1 with
-    # a gather, GPU 0's assembled buffers vs a local forward of hands
+    # on every rank, sampled hands of its shard vs the float64 oracle in a
+    # child process (rank 0 reports the max over ranks), and at N > 1 with a
+    # gather, GPU 0's assembled buffers vs a local forward of hands
     # regenerated by global index from every rank's range.
     correctness, gather_check = None, None
     device_status = model.device_status(clear=True)  # MANO_DEVICE_* bits raised by any launch (0 = none)
-    if rank == 0 and not args.no_check:
+    if not args.no_check:
         correctness = check_sample(model, wl["seed"], rank * B, B, betas, pose, trans, verts, joints,
                                    args.model, with_trans)
+        correctness["device_status"] = device_status
+        correctness["pass"] = bool(correctness.get("pass")) and device_status == 0
+        if world > 1:
+            per_rank = [None] * world
+            dist.all_gather_object(per_rank, correctness)
+            correctness = merge_checks(per_rank)
+    elif world > 1:
+        st = [None] * world
+        dist.all_gather_object(st, device_status)
+        device_status = max(st)
+    if correctness is not None:
+        device_status = correctness.get("device_status", device_status)
     if rank == 0 and gv is not None:
         gather_check = check_gather(model, wl["seed"], B, world, gv, gj, with_trans)
         if args.dump_gather:

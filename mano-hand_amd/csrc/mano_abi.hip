@@ -366,26 +366,6 @@ int mano_forward(const mano_model* m, int64_t n, const float* betas, int64_t bet
   g_last_error.clear();
   if (int rc = check_model(m)) return rc;
   if (n > 0 && !verts) return fail(MANO_EINVAL, "verts is required");
-  if (!rest_verts && !rest_joints && !rot_mats && m->dm.precision == MANO_PRECISION_FP32) {
-    // verts (+ joints, trans): one launch, the articulation inside the fused
-    // blend GEMM + LBS kernel (launch_forward_fused)
-    if (n < 0 || n > kMaxHands) return fail(MANO_EINVAL, "n_hands %lld out of range", (long long)n);
-    if (n == 0) return MANO_OK;
-    if (!betas || !pose) return fail(MANO_EINVAL, "betas and pose are required");
-    if (betas_stride != 0 && betas_stride < mano::kShape)
-      return fail(MANO_EINVAL, "betas_stride %lld must be 0 or >= 10", (long long)betas_stride);
-    if (int rc = check_workspace(m, n, ws, ws_bytes, false)) return rc;
-    DeviceGuard guard(m->device);
-    if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
-    const mano::Workspace w = mano::workspace_layout(m->dm, n);
-    char* base = static_cast<char*>(ws);
-    hipError_t e = mano::launch_forward_fused(
-        m->dm, n, betas, betas_stride, pose, trans, verts, joints,
-        reinterpret_cast<float*>(base + w.features_off), reinterpret_cast<float*>(base + w.transforms_off),
-        static_cast<hipStream_t>(stream));
-    if (e != hipSuccess) return hip_fail(e, "forward launch");
-    return MANO_OK;
-  }
   if (int rc = mano_stage_articulate(m, n, betas, betas_stride, pose, trans, joints, rest_joints,
                                      rot_mats, ws, ws_bytes, stream))
     return rc;

@@ -77,13 +77,6 @@ hipError_t launch_blend(const DeviceModel& m, int64_t n, const float* features,
 hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features,
                              const float* transforms, const float* trans, float* verts,
                              float* vposed, hipStream_t stream);
-// mano_forward in one launch (verts, joints, trans; fp32): blend_skin16 with
-// the articulation in its range prologue, the X rows / transforms workspace
-// written and read by the kernel itself.
-hipError_t launch_forward_fused(const DeviceModel& m, int64_t n, const float* betas,
-                                int64_t betas_stride, const float* pose, const float* trans,
-                                float* verts, float* joints, float* features, float* transforms,
-                                hipStream_t stream);
 hipError_t launch_skin(const DeviceModel& m, int64_t n, const float* transforms,
                        const float* vposed, const float* trans, float* verts,
                        hipStream_t stream);

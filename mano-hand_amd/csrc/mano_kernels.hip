@@ -19,7 +19,6 @@
 #include <algorithm>
 
 #include "mano_internal.h"
-#include "mano_joint.h"
 #include "mano_span.h"
 
 namespace mano {
@@ -346,38 +345,12 @@ __device__ __forceinline__ void bs_stamp(int slot, unsigned long long v) {
 #ifndef MANO_BS_BLOCKS_PER_CU
 #define MANO_BS_BLOCKS_PER_CU 3  // resident blocks per CU (diagnostic builds: 1, 2, 4)
 #endif
-// The single-launch forward (kArt): blend_skin16 articulates each hand tile
-// itself at the start of every range of its units -- articulate_kernel's lane
-// per (hand, joint), 4 rounds of 4 hands per wave (mano_joint.h), the X rows
-// and transforms written to the workspace exactly as articulate_kernel writes
-// them and read straight back by the same wave (L2), posed joints written by
-// the block that owns the tile set's first vertex group.  The articulation's
-// HBM writes (1.4 KB per hand) then drain behind the MFMA work instead of
-// forming a launch of their own.
-struct ArtArgs {
-  const float* betas;
-  int64_t betas_stride;
-  const float* pose;
-  const float* joint_template;  // [16][3]
-  const float* joint_shape;     // [16][3][10]
-  const int32_t* parents;
-  const int32_t* depth;
-  int max_depth;
-  float* joints;                // nullable: posed joints (+ trans)
-  float* features;              // workspace X rows (written, then read back)
-  float* transforms;            // workspace transforms (written, then read back)
-};
-
-template <bool kTrans, bool kVposed, bool kArt = false>
+template <bool kTrans, bool kVposed>
 __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kernel(
-    const float* __restrict__ features_in, const float* __restrict__ transforms_in,
+    const float* __restrict__ features, const float* __restrict__ transforms,
     const float* __restrict__ basis16, const float* __restrict__ wfrag16,
     const float* __restrict__ trans, float* __restrict__ verts, float* __restrict__ vposed,
-    int64_t n, int n_verts, int n_groups, ArtArgs art) {
-  // kArt: the X rows / transforms are this kernel's own output, so they are
-  // read through plain (aliasing) pointers, never as const __restrict__.
-  const float* features = kArt ? art.features : features_in;
-  const float* transforms = kArt ? art.transforms : transforms_in;
+    int64_t n, int n_verts, int n_groups) {
   // One slot: a basis tile (10 KB) + the group's W fragment (1 KB, with the
   // group's first tile); ring of 3.
   constexpr int kRingF4 = (kGroups16 + 1) * 64;
@@ -388,31 +361,14 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
   // group's first tile, the previous group's stores.
   constexpr int kPieces = kGroups16 / 4;     // LDS-DMA pieces per wave and tile, at least
   constexpr int kDmaPrio = MANO_BS_DMA_PRIO, kStorePrio = MANO_BS_STORE_PRIO;
-  constexpr int kJtJs = kJoints * 3 + kJoints * 3 * kShape;  // folded joint regressor, 528 floats
-  // kArt: the folded regressor sits behind the ring in the same array (a
-  // second LDS array made hipcc wait vmcnt(0) for the ring's DMA before
-  // every LDS read of the group loop)
-  __shared__ f32x4 lds[kSlots * kRingF4 + (kArt ? kJtJs / 4 : 0)];
+  __shared__ f32x4 lds[kSlots * kRingF4];
   __shared__ float trs[4][16 * 3];  // the wave's 16 translations, read back at the stores
-  float* const jreg_s = reinterpret_cast<float*>(lds + kSlots * kRingF4);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int vstride32 = 3 * n_verts;
   const int64_t nt16 = (n + 15) / 16;
   const int64_t n_quads = (nt16 + 3) / 4;
   int64_t u, u_end;
   unit_range(n_quads * n_groups, blockIdx.x, gridDim.x, u, u_end);
-  int art_src = 0, art_dep = 0;
-  if constexpr (kArt) {
-    // once per block: the folded regressor (J = Jt + Js . beta) into LDS and
-    // this lane's joint's parent lane and tree depth (lane & 15 = joint)
-    for (int i = threadIdx.x; i < kJtJs; i += 256)
-      jreg_s[i] = i < kJoints * 3 ? art.joint_template[i] : art.joint_shape[i - kJoints * 3];
-    const int j = threadIdx.x & 15;
-    const int par = art.parents[j];
-    art_src = ((threadIdx.x & 63) & ~15) + (par < 0 ? 0 : par);
-    art_dep = art.depth[j];
-    __syncthreads();
-  }
 #if MANO_BS_STAMP
   bs_stamp(0, __builtin_amdgcn_s_memtime());
   bs_stamp(2, __builtin_amdgcn_s_memrealtime());
@@ -445,49 +401,6 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
     const int row0 = 4 * (lane >> 4);  // D rows (hands) of this lane: row0 + r
     const int col = lane & 15;         // D column (vertex of the group)
 
-    if constexpr (kArt) {
-      // Articulate the wave's 16 hands: round r takes hands 4r .. 4r + 3, a
-      // lane per (hand, joint), exactly articulate_kernel's arithmetic and
-      // output layout (rows past the batch end repeat the last hand, as the
-      // A-fragment loads below do, so every store is of identical values).
-      const int j = lane & 15;
-      const bool own_joints = art.joints != nullptr && g0 == 0;  // one block per tile set
-#pragma unroll 1
-      for (int r = 0; r < 4; ++r) {
-        const int64_t hh = h0 + 4 * r + (lane >> 4);
-        const int64_t h = hh < n ? hh : n - 1;
-        const float* pp = art.pose + h * (kJoints * 3) + 3 * j;
-        const float ax = pp[0], ay = pp[1], az = pp[2];
-        float beta[kShape];
-#pragma unroll
-        for (int k = 0; k < kShape; ++k) beta[k] = art.betas[h * art.betas_stride + k];
-        float rm[9], J[3], t[3], Aj[12];
-        articulate_joint(ax, ay, az, beta, j, art_src, art_dep, art.max_depth, jreg_s,
-                         jreg_s + kJoints * 3, rm, J, t, Aj);
-        f32x4* A = reinterpret_cast<f32x4*>(art.transforms + h * kTransformFloats + j * 12);
-        A[0] = f32x4{Aj[0], Aj[1], Aj[2], Aj[3]};
-        A[1] = f32x4{Aj[4], Aj[5], Aj[6], Aj[7]};
-        A[2] = f32x4{Aj[8], Aj[9], Aj[10], Aj[11]};
-        float* x = art.features + h * kXStride;
-        if (j == 0) {
-#pragma unroll
-          for (int k = 0; k < kShape; ++k) x[x_pos(k)] = beta[k];
-          x[x_pos(kK)] = 1.f;
-#pragma unroll
-          for (int k = kK + 1; k < kXStride; ++k) x[x_pos(k)] = 0.f;
-        } else {
-#pragma unroll
-          for (int m = 0; m < 9; ++m) x[x_pos(kShape + 9 * (j - 1) + m)] = rm[m];
-        }
-        if (own_joints && hh < n) {
-          float* o = art.joints + hh * (kJoints * 3) + 3 * j;
-#pragma unroll
-          for (int c = 0; c < 3; ++c) o[c] = t[c] + (kTrans ? trans[hh * 3 + c] : 0.f);
-        }
-      }
-      // the rows and transforms are in L2 before this wave reads them back
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
 
     float a[kGroups16 * 4];
     float F[12][4];  // LBS A fragments, tile (c, k) = c * 4 + k, resident for the quad
@@ -950,7 +863,7 @@ hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* featu
   auto launch = [&](auto kernel) {
     hipLaunchKernelGGL(kernel, persistent_grid(kernel, m, n_quads * m.n_groups16, 1, kBlendSkinBlocksPerCU),
                        dim3(256), 0, stream, features, transforms, m.basis16, m.wfrag16, trans, verts,
-                       vposed, n, m.n_verts, m.n_groups16, ArtArgs{});
+                       vposed, n, m.n_verts, m.n_groups16);
   };
 #if MANO_BS_WIDE
   const int64_t n_sets = ((n + 15) / 16 + kWideWaves - 1) / kWideWaves;
@@ -973,26 +886,6 @@ hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* featu
   else if (trans) launch(blend_skin16_kernel<true, false>);
   else if (vposed) launch(blend_skin16_kernel<false, true>);
   else launch(blend_skin16_kernel<false, false>);
-  return hipGetLastError();
-}
-
-// The single-launch forward: blend_skin16 with the articulation in its range
-// prologue (kArt).  The workspace's X rows and transforms are written and read
-// by the kernel itself.
-hipError_t launch_forward_fused(const DeviceModel& m, int64_t n, const float* betas,
-                                int64_t betas_stride, const float* pose, const float* trans,
-                                float* verts, float* joints, float* features, float* transforms,
-                                hipStream_t stream) {
-  const int64_t n_quads = ((n + 15) / 16 + 3) / 4;
-  const ArtArgs art{betas, betas_stride, pose, m.joint_template, m.joint_shape, m.parents, m.depth,
-                    m.max_depth, joints, features, transforms};
-  auto launch = [&](auto kernel) {
-    hipLaunchKernelGGL(kernel, persistent_grid(kernel, m, n_quads * m.n_groups16, 1, kBlendSkinBlocksPerCU),
-                       dim3(256), 0, stream, nullptr, nullptr, m.basis16, m.wfrag16, trans, verts, nullptr,
-                       n, m.n_verts, m.n_groups16, art);
-  };
-  if (trans) launch(blend_skin16_kernel<true, false, true>);
-  else launch(blend_skin16_kernel<false, false, true>);
   return hipGetLastError();
 }
 

@@ -92,3 +92,26 @@ def test_pmc_values_parse(tmp_path):
     assert bench.pmc_values(str(tmp_path), "FETCH_SIZE", frag) == [100.0, 300.0]
     assert bench.pmc_values(str(tmp_path), "WRITE_SIZE", frag) == [9.0]
     assert bench.pmc_values(str(tmp_path), "FETCH_SIZE", bench.PMC_KERNEL_NAME["blend_skin_h3"]) == []
+
+
+def test_merge_checks_takes_the_worst_rank():
+    """bench.py's per-rank correctness legs merge into one rank-0 summary."""
+    a = {"max_abs_err_verts": 1e-7, "max_abs_err_joints": 5e-8, "n_sampled": 60, "pass": True,
+         "finite": True, "device_status": 0, "worst_hand_verts": 3}
+    b = {"max_abs_err_verts": 2e-7, "max_abs_err_joints": 1e-8, "n_sampled": 62, "pass": True,
+         "finite": True, "device_status": 0, "worst_hand_verts": 70000}
+    m = bench.merge_checks([a, b])
+    assert m["max_abs_err_verts"] == 2e-7 and m["max_abs_err_joints"] == 5e-8
+    assert m["n_sampled"] == 122 and m["ranks_checked"] == 2 and m["pass"]
+    assert m["worst_hand_verts"] == 70000
+    bad = dict(b, **{"pass": False, "device_status": 1})
+    m = bench.merge_checks([a, bad])
+    assert not m["pass"] and m["device_status"] == 1
+    assert "error" in bench.merge_checks([a, {"error": "x"}])
+
+
+def test_sample_indices_cover_edges():
+    idx = bench.sample_indices(65536)
+    for h in (0, 15, 16, 63, 64, 32767, 32768, 65535):
+        assert h in idx
+    assert bench.sample_indices(3).tolist() == [0, 1, 2]

@@ -405,42 +405,6 @@ def test_forward_equals_staged(engine, dev, params, B, shared, with_trans):
     assert np.abs(host(one["joints"]) - ref["joints"]).max() <= TOL_M
 
 
-@pytest.mark.parametrize("B,shared,with_trans,joints", [(1, False, True, True), (17, True, False, True),
-                                                        (200, False, False, False), (4096, False, True, True),
-                                                        (65537, False, False, True)])
-def test_single_launch_forward_equals_staged(engine, dev, params, B, shared, with_trans, joints):
-    """mano_forward with only verts (+ joints, trans) is ONE launch: blend_skin16
-    articulating each hand tile in its range prologue.  Its verts and joints,
-    and the X rows / transforms it leaves in the workspace, equal the staged
-    articulate + blend_skin16 bit for bit (ragged batches, shared betas)."""
-    rng = np.random.default_rng(700 + B)
-    betas = f32(rng.normal(0, 1, (10,) if shared else (B, 10)), dev)
-    pose = f32(rng.normal(0, 0.6, (B, 16, 3)), dev)
-    trans = f32(rng.uniform(-1, 1, (B, 3)), dev) if with_trans else None
-    one = engine.forward(betas, pose, trans, joints=joints)
-    torch.cuda.synchronize()
-    ws = engine.intermediates(B)
-    x1, t1 = ws["features"].clone(), ws["transforms"].clone()
-    j = torch.empty((B, 16, 3), device=dev)
-    v = torch.empty((B, 778, 3), device=dev)
-    engine.stage_articulate(betas, pose, trans, joints=j)
-    engine.stage_blend_skin(B, v, trans=trans)
-    torch.cuda.synchronize()
-    ws = engine.intermediates(B)
-    assert torch.equal(x1, ws["features"]) and torch.equal(t1, ws["transforms"])
-    assert torch.equal(one["verts"], v)
-    if joints:
-        assert torch.equal(one["joints"], j)
-    b = host(betas)
-    idx = np.unique(np.r_[0, B - 1, np.random.default_rng(B).integers(0, B, 64)])
-    ref = mano_oracle.forward(params, (np.broadcast_to(b, (B, 10)) if shared else b)[idx], host(pose)[idx],
-                              None if trans is None else host(trans)[idx])
-    assert np.abs(host(one["verts"])[idx] - ref["verts"]).max() <= TOL_M
-    if joints:
-        assert np.abs(host(one["joints"])[idx] - ref["joints"]).max() <= TOL_M
-    engine.check_device()
-
-
 def truncated_params(params, V):
     """The synthetic model cut to its first V vertices: a smaller mesh of the
     same layout (exercises every span / tail-group case of the kernels)."""
@@ -469,13 +433,11 @@ def test_other_mesh_sizes(dev, params, V, precision):
         pose = f32(rng.normal(0, 0.6, (B, 16, 3)), dev)
         trans = f32(rng.uniform(-1, 1, (B, 3)), dev)
         fused = m.forward(betas, pose, trans, joints=True, rest_verts=True)
-        one = m.forward(betas, pose, trans, joints=True)  # fp32: the single-launch forward
         m.stage_articulate(betas, pose, trans)
         v = torch.empty((B, V, 3), device=dev)
         m.stage_skin(B, v, rest_verts=fused["rest_verts"], trans=trans)
         torch.cuda.synchronize()
         assert torch.equal(fused["verts"], v)
-        assert torch.equal(one["verts"], fused["verts"]) and torch.equal(one["joints"], fused["joints"])
         ref = mano_oracle.forward(p, host(betas), host(pose), host(trans))
         for key in ("verts", "joints", "rest_verts"):
             err = np.abs(host(fused[key]) - ref[key]).max()

@@ -52,6 +52,13 @@ a, b, s = steps([art, lambda: m.stage_blend(B), lambda: m.stage_skin(B, v)])
 res["unfused"] = {"articulate": a, "blend": b, "skin": s}
 res["unfused_digest"] = digest(v)
 res["skin_b2b"] = steps([lambda: m.stage_skin(B, v)])[0]
+# the same step with 1 GiB of unrelated copies between the blend GEMM and the
+# LBS: if the LBS's in-path penalty is the blend's dirty v_posed lines in the
+# caches, the flush moves it into the copy
+fa = torch.empty(1 << 28, device="cuda:0"); fb = torch.empty_like(fa)
+a, b, c, s2 = steps([art, lambda: m.stage_blend(B), lambda: fb.copy_(fa), lambda: m.stage_skin(B, v)], reps=50)
+res["unfused_flushed"] = {"blend": b, "copy": c, "skin": s2}
+del fa, fb
 a, f = steps([art, lambda: m.stage_blend_skin(B, v)])
 res["fused"] = {"articulate": a, "blend_skin": f, "step": a + f}
 res["fused_digest"] = digest(v)
