@@ -26,6 +26,7 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));  // hand rows: 8-B aligned for odd hands
 
 
 // ---------------------------------------------------------------------------
@@ -345,6 +346,13 @@ __device__ __forceinline__ void bs_stamp(int slot, unsigned long long v) {
 #ifndef MANO_BS_BLOCKS_PER_CU
 #define MANO_BS_BLOCKS_PER_CU 3  // resident blocks per CU (diagnostic builds: 1, 2, 4)
 #endif
+// Verts leave through a per-wave LDS stage: the lanes drop their 12-B points
+// into the 16 hand rows (48 floats each), then read them back as float4 and
+// store 3 dwordx4 per lane (1 KB per instruction) instead of 4 dwordx3.
+#ifndef MANO_BS_STAGED_STORE
+#define MANO_BS_STAGED_STORE 0
+#endif
+constexpr int kStageRow = 52;  // floats per staged hand row (48 + pad: conflict-free float4 reads)
 template <bool kTrans, bool kVposed>
 __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kernel(
     const float* __restrict__ features, const float* __restrict__ transforms,
@@ -355,13 +363,18 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
   // group's first tile); ring of 3.
   constexpr int kRingF4 = (kGroups16 + 1) * 64;
   constexpr int kSlots = 3;
-  constexpr int kStores = (MANO_BS_ABLATE & 1) ? 0 : kVposed ? 8 : 4;  // global_store_dwordx3 per group
+  constexpr int kVertStores = MANO_BS_STAGED_STORE ? 3 : 4;  // verts stores per group (dwordx4 / dwordx3)
+  constexpr int kStores = (MANO_BS_ABLATE & 1) ? 0 : kVertStores + (kVposed ? 4 : 0);
   // vmcnt of the barrier after tile t: the wave's memory ops issued after tile
   // t + 1's DMA -- tile t + 2's DMA (at least 2 pieces per wave) and, after a
   // group's first tile, the previous group's stores.
   constexpr int kPieces = kGroups16 / 4;     // LDS-DMA pieces per wave and tile, at least
   constexpr int kDmaPrio = MANO_BS_DMA_PRIO, kStorePrio = MANO_BS_STORE_PRIO;
-  __shared__ f32x4 lds[kSlots * kRingF4];
+  // (the verts stage, when used, sits behind the ring in the same array: a
+  // second LDS array makes hipcc wait vmcnt(0) -- the ring's DMA -- before
+  // the group loop's LDS reads)
+  constexpr int kStageF4 = MANO_BS_STAGED_STORE ? 16 * kStageRow / 4 : 0;  // per wave
+  __shared__ f32x4 lds[kSlots * kRingF4 + 4 * kStageF4];
   __shared__ float trs[4][16 * 3];  // the wave's 16 translations, read back at the stores
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int vstride32 = 3 * n_verts;
@@ -493,6 +506,37 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
         continue;
       }
       prio_up<kStorePrio>();
+      if constexpr (MANO_BS_STAGED_STORE) {
+        // Rows into the stage, then 3 float4 per lane: float4 i of the
+        // wave's 192 is row (64 m + lane) / 12, column 4 ((64 m + lane) % 12).
+        float* st = reinterpret_cast<float*>(lds + kSlots * kRingF4 + wave * kStageF4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int hr = row0 + r;
+          float o0 = out[0][r], o1 = out[1][r], o2 = out[2][r];
+          if constexpr (kTrans) {
+            const int ht = min(hr, n_valid - 1);
+            o0 += trs[wave][ht * 3 + 0];
+            o1 += trs[wave][ht * 3 + 1];
+            o2 += trs[wave][ht * 3 + 2];
+          }
+          st[hr * kStageRow + 3 * col + 0] = o0;
+          st[hr * kStageRow + 3 * col + 1] = o1;
+          st[hr * kStageRow + 3 * col + 2] = o2;
+          if constexpr (kVposed)
+            store_out<false>(ptile + unsigned(min(hr, n_valid - 1) * vstride32 + voff),
+                             f32x3{p[0][r], p[1][r], p[2][r]});
+        }
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+          const int i = 64 * m + lane;
+          const int hr = min(i / 12, n_valid - 1), c4 = 4 * (i % 12);  // rows past the batch: the last hand again
+          const f32x4 v = *reinterpret_cast<const f32x4*>(st + hr * kStageRow + c4);
+          float* dst = vtile + unsigned(hr * vstride32 + 3 * vb + c4);
+          if constexpr (MANO_BS_NT_STORE && !kVposed) __builtin_nontemporal_store(v, reinterpret_cast<f32x4u*>(dst));
+          else *reinterpret_cast<f32x4u*>(dst) = v;
+        }
+      } else {
       // One 12-B point store per row; rows past the batch end rewrite the
       // last hand's identical values.
 #pragma unroll
@@ -510,6 +554,7 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
           store_out<MANO_BS_NT_STORE && !kVposed>(vtile + unsigned(hr * vstride32 + voff), f32x3{o0, o1, o2});
         if constexpr (kVposed)
           store_out<false>(ptile + unsigned(hr * vstride32 + voff), f32x3{p[0][r], p[1][r], p[2][r]});
+      }
       }
       prio_down<kStorePrio>();
     }
