@@ -98,12 +98,65 @@ __device__ __forceinline__ void stage_basis_tile16(const float* __restrict__ bas
   }
 }
 
+// v_posed of one finished 32-hand x 32-column tile through the wave's LDS stage
+// as 32-B-aligned float4 windows (blend_skin16's store_staged, for the
+// unfused GEMM's 32x32 tiles): each hand row's window [first byte - c, +128)
+// starts on a sector boundary and carries the previous tile's last c floats,
+// which stay in the row's carry area [8 - c, 8) of the stage.  4 dwordx4 per
+// lane instead of 16 dword stores; the first tile of a row (no carry) and the
+// last (clipped at the row end) keep the plain window / element stores.
+#ifndef MANO_BLEND_STAGED
+#define MANO_BLEND_STAGED 1
+#endif
+constexpr int kBlendStageRow = 48;  // floats: [8 carry | 32 data | 8 pad]
+__device__ __forceinline__ void store_vposed_staged(float* __restrict__ vposed, float* st, const f32x16& acc,
+                                                    int64_t h0, int t, int64_t n, int n_cols, int n_col_tiles,
+                                                    int lane) {
+  const int hi = lane >> 5, col = lane & 31;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) st[((r & 3) + 8 * (r >> 2) + 4 * hi) * kBlendStageRow + 8 + col] = acc[r];
+  const int col0 = t * kColTile;
+  const bool last = t + 1 == n_col_tiles;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int i = 64 * m + lane, row = i >> 3, f4 = i & 7;
+    const int64_t h = h0 + row;
+    if (h < n) {
+      float* row_ptr = vposed + h * n_cols;
+      const int c = t > 0 ? int((reinterpret_cast<uintptr_t>(row_ptr) >> 2) & 7) : 0;
+      const float* sp = st + row * kBlendStageRow + 8 - c + 4 * f4;
+      const int cc = col0 - c + 4 * f4;  // first column of this float4
+      if (!last || cc + 4 <= n_cols) {
+        *reinterpret_cast<f32x4u*>(row_ptr + cc) = f32x4{sp[0], sp[1], sp[2], sp[3]};
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (cc + e < n_cols) row_ptr[cc + e] = sp[e];
+      }
+    }
+  }
+  // each row's last c floats are the next tile's carry
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int idx = 64 * k + lane, row = idx >> 3, e = idx & 7;
+    const int64_t h = min(h0 + row, n - 1);
+    const int c = int((reinterpret_cast<uintptr_t>(vposed + h * n_cols) >> 2) & 7);
+    if (e < c) st[row * kBlendStageRow + 8 - c + e] = st[row * kBlendStageRow + 40 - c + e];
+  }
+}
+
 __global__ __launch_bounds__(256, 2) void blend_kernel(
     const float* __restrict__ features, const float* __restrict__ basis_tiles,
     float* __restrict__ vposed, int64_t n, int n_cols, int n_col_tiles) {
-  __shared__ f32x4 bs[2][kKGroups * 64];
+  // the basis double buffer, then (staged stores) the 4 waves' v_posed stages
+  // in the same array (a second LDS array made hipcc wait for the DMA)
+  constexpr int kStageF4 = MANO_BLEND_STAGED ? 32 * kBlendStageRow / 4 : 0;
+  __shared__ f32x4 bs_all[2 * kKGroups * 64 + 4 * kStageF4];
+  auto bs = [&](int i) { return bs_all + i * (kKGroups * 64); };
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float* st = reinterpret_cast<float*>(bs_all + 2 * kKGroups * 64 + wave * kStageF4);
+  (void)st;
   const int64_t ht = int64_t(blockIdx.x) * 4 + wave;
   const int64_t n_ht = (n + kHandTile - 1) / kHandTile;
   const bool active = ht < n_ht;
@@ -118,7 +171,7 @@ __global__ __launch_bounds__(256, 2) void blend_kernel(
     for (int s = 0; s < kKGroups * 4; ++s) a[s] = s < kKSteps ? x[x_pos(2 * s + (lane >> 5))] : 0.f;
   }
 
-  stage_basis_tile(basis_tiles, 0, bs[0], wave, lane);
+  stage_basis_tile(basis_tiles, 0, bs(0), wave, lane);
   __syncthreads();
 
   const int hi = lane >> 5;
@@ -130,12 +183,18 @@ __global__ __launch_bounds__(256, 2) void blend_kernel(
   // stores and the DMA the MFMA chain has already hidden.
   f32x16 prev = {};
   for (int t = 0; t < n_col_tiles; ++t) {
-    if (active && t > 0) store_vposed_tile(vposed, prev, h0, (t - 1) * kColTile + col_in_tile, n, n_cols, hi);
-    if (t + 1 < n_col_tiles) stage_basis_tile(basis_tiles, t + 1, bs[(t + 1) & 1], wave, lane);
-    prev = mfma_tile(a, bs[t & 1], lane);
+    if (active && t > 0) {
+      if constexpr (MANO_BLEND_STAGED) store_vposed_staged(vposed, st, prev, h0, t - 1, n, n_cols, n_col_tiles, lane);
+      else store_vposed_tile(vposed, prev, h0, (t - 1) * kColTile + col_in_tile, n, n_cols, hi);
+    }
+    if (t + 1 < n_col_tiles) stage_basis_tile(basis_tiles, t + 1, bs((t + 1) & 1), wave, lane);
+    prev = mfma_tile(a, bs(t & 1), lane);
     __syncthreads();
   }
-  if (active) store_vposed_tile(vposed, prev, h0, (n_col_tiles - 1) * kColTile + col_in_tile, n, n_cols, hi);
+  if (active) {
+    if constexpr (MANO_BLEND_STAGED) store_vposed_staged(vposed, st, prev, h0, n_col_tiles - 1, n, n_cols, n_col_tiles, lane);
+    else store_vposed_tile(vposed, prev, h0, (n_col_tiles - 1) * kColTile + col_in_tile, n, n_cols, hi);
+  }
 }
 
 // ---------------------------------------------------------------------------
