@@ -98,3 +98,34 @@ def test_pca_branch(params, n):
     pose = mano_oracle.pose_from_pca(params, c, rot)[0]
     ref = (c @ params["pose_pca_basis"][:n] + params["pose_pca_mean"]).reshape(15, 3)
     assert np.allclose(pose[1:], ref) and np.allclose(pose[0], rot)
+
+
+def test_check_sample_leg(tmp_path):
+    """bench.py's correctness leg (oracle/check_sample.py, run as a child
+    process by the bench): exact oracle outputs read as ~0 error, a 2e-5 m
+    perturbation of one hand is found and reported with its global index."""
+    import json
+    import subprocess
+    import sys
+    from mano_amd.model_io import synthetic_params
+    from oracle import mano_oracle
+    from conftest import REPO
+    rng = np.random.default_rng(3)
+    n = 7
+    betas = rng.normal(0, 1, (n, 10)).astype(np.float32)
+    pose = rng.normal(0, 0.5, (n, 16, 3)).astype(np.float32)
+    trans = rng.uniform(-1, 1, (n, 3)).astype(np.float32)
+    ref = mano_oracle.forward(synthetic_params(0), betas.astype(np.float64), pose.astype(np.float64),
+                              trans.astype(np.float64))
+    verts = ref["verts"].astype(np.float64)
+    verts[4, 100, 1] += 2e-5
+    path = tmp_path / "s.npz"
+    np.savez(path, index=np.arange(1000, 1000 + n), betas=betas, pose=pose, trans=trans, verts=verts,
+             joints=ref["joints"], model=np.array("synthetic:0"))
+    r = subprocess.run([sys.executable, f"{REPO}/oracle/check_sample.py", str(path)], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["n_sampled"] == n and res["finite"]
+    assert 1.5e-5 < res["max_abs_err_verts"] < 2.5e-5 and res["worst_hand_verts"] == 1004
+    assert res["max_abs_err_joints"] < 1e-12
