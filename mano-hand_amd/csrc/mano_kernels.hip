@@ -98,65 +98,12 @@ __device__ __forceinline__ void stage_basis_tile16(const float* __restrict__ bas
   }
 }
 
-// v_posed of one finished 32-hand x 32-column tile through the wave's LDS stage
-// as 32-B-aligned float4 windows (blend_skin16's store_staged, for the
-// unfused GEMM's 32x32 tiles): each hand row's window [first byte - c, +128)
-// starts on a sector boundary and carries the previous tile's last c floats,
-// which stay in the row's carry area [8 - c, 8) of the stage.  4 dwordx4 per
-// lane instead of 16 dword stores; the first tile of a row (no carry) and the
-// last (clipped at the row end) keep the plain window / element stores.
-#ifndef MANO_BLEND_STAGED
-#define MANO_BLEND_STAGED 1
-#endif
-constexpr int kBlendStageRow = 48;  // floats: [8 carry | 32 data | 8 pad]
-__device__ __forceinline__ void store_vposed_staged(float* __restrict__ vposed, float* st, const f32x16& acc,
-                                                    int64_t h0, int t, int64_t n, int n_cols, int n_col_tiles,
-                                                    int lane) {
-  const int hi = lane >> 5, col = lane & 31;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) st[((r & 3) + 8 * (r >> 2) + 4 * hi) * kBlendStageRow + 8 + col] = acc[r];
-  const int col0 = t * kColTile;
-  const bool last = t + 1 == n_col_tiles;
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const int i = 64 * m + lane, row = i >> 3, f4 = i & 7;
-    const int64_t h = h0 + row;
-    if (h < n) {
-      float* row_ptr = vposed + h * n_cols;
-      const int c = t > 0 ? int((reinterpret_cast<uintptr_t>(row_ptr) >> 2) & 7) : 0;
-      const float* sp = st + row * kBlendStageRow + 8 - c + 4 * f4;
-      const int cc = col0 - c + 4 * f4;  // first column of this float4
-      if (!last || cc + 4 <= n_cols) {
-        *reinterpret_cast<f32x4u*>(row_ptr + cc) = f32x4{sp[0], sp[1], sp[2], sp[3]};
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (cc + e < n_cols) row_ptr[cc + e] = sp[e];
-      }
-    }
-  }
-  // each row's last c floats are the next tile's carry
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int idx = 64 * k + lane, row = idx >> 3, e = idx & 7;
-    const int64_t h = min(h0 + row, n - 1);
-    const int c = int((reinterpret_cast<uintptr_t>(vposed + h * n_cols) >> 2) & 7);
-    if (e < c) st[row * kBlendStageRow + 8 - c + e] = st[row * kBlendStageRow + 40 - c + e];
-  }
-}
-
 __global__ __launch_bounds__(256, 2) void blend_kernel(
     const float* __restrict__ features, const float* __restrict__ basis_tiles,
     float* __restrict__ vposed, int64_t n, int n_cols, int n_col_tiles) {
-  // the basis double buffer, then (staged stores) the 4 waves' v_posed stages
-  // in the same array (a second LDS array made hipcc wait for the DMA)
-  constexpr int kStageF4 = MANO_BLEND_STAGED ? 32 * kBlendStageRow / 4 : 0;
-  __shared__ f32x4 bs_all[2 * kKGroups * 64 + 4 * kStageF4];
-  auto bs = [&](int i) { return bs_all + i * (kKGroups * 64); };
+  __shared__ f32x4 bs[2][kKGroups * 64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  float* st = reinterpret_cast<float*>(bs_all + 2 * kKGroups * 64 + wave * kStageF4);
-  (void)st;
   const int64_t ht = int64_t(blockIdx.x) * 4 + wave;
   const int64_t n_ht = (n + kHandTile - 1) / kHandTile;
   const bool active = ht < n_ht;
@@ -171,7 +118,7 @@ __global__ __launch_bounds__(256, 2) void blend_kernel(
     for (int s = 0; s < kKGroups * 4; ++s) a[s] = s < kKSteps ? x[x_pos(2 * s + (lane >> 5))] : 0.f;
   }
 
-  stage_basis_tile(basis_tiles, 0, bs(0), wave, lane);
+  stage_basis_tile(basis_tiles, 0, bs[0], wave, lane);
   __syncthreads();
 
   const int hi = lane >> 5;
@@ -183,18 +130,12 @@ __global__ __launch_bounds__(256, 2) void blend_kernel(
   // stores and the DMA the MFMA chain has already hidden.
   f32x16 prev = {};
   for (int t = 0; t < n_col_tiles; ++t) {
-    if (active && t > 0) {
-      if constexpr (MANO_BLEND_STAGED) store_vposed_staged(vposed, st, prev, h0, t - 1, n, n_cols, n_col_tiles, lane);
-      else store_vposed_tile(vposed, prev, h0, (t - 1) * kColTile + col_in_tile, n, n_cols, hi);
-    }
-    if (t + 1 < n_col_tiles) stage_basis_tile(basis_tiles, t + 1, bs((t + 1) & 1), wave, lane);
-    prev = mfma_tile(a, bs(t & 1), lane);
+    if (active && t > 0) store_vposed_tile(vposed, prev, h0, (t - 1) * kColTile + col_in_tile, n, n_cols, hi);
+    if (t + 1 < n_col_tiles) stage_basis_tile(basis_tiles, t + 1, bs[(t + 1) & 1], wave, lane);
+    prev = mfma_tile(a, bs[t & 1], lane);
     __syncthreads();
   }
-  if (active) {
-    if constexpr (MANO_BLEND_STAGED) store_vposed_staged(vposed, st, prev, h0, n_col_tiles - 1, n, n_cols, n_col_tiles, lane);
-    else store_vposed_tile(vposed, prev, h0, (n_col_tiles - 1) * kColTile + col_in_tile, n, n_cols, hi);
-  }
+  if (active) store_vposed_tile(vposed, prev, h0, (n_col_tiles - 1) * kColTile + col_in_tile, n, n_cols, hi);
 }
 
 // ---------------------------------------------------------------------------
@@ -405,71 +346,13 @@ __device__ __forceinline__ void bs_stamp(int slot, unsigned long long v) {
 #ifndef MANO_BS_BLOCKS_PER_CU
 #define MANO_BS_BLOCKS_PER_CU 3  // resident blocks per CU (diagnostic builds: 1, 2, 4)
 #endif
-// Output rows through a per-wave LDS stage, 32-B-aligned windows.  A group's
-// 16 x 16 points leave as 4 point stores (dwordx3: 192 B per hand row, which
-// for 3 hands in 4 starts and ends inside a 32-B sector that the next group
-// of the same wave completes).  Staged, the lanes drop their points into the
-// stage's 16 hand rows, then store each row's window [first byte - c, +192)
-// as float4s, c = the row's offset past a 32-B boundary: the window starts
-// on a sector boundary and carries the previous group's last c bytes (kept
-// in a per-stream carry area of the stage), so inside a range no sector is
-// written in two pieces.  The first group of a range and the mesh's shifted
-// last group use the unshifted window (their carry is not at hand).  3
-// dwordx4 per lane and stream instead of 4 dwordx3.  Measured (65,536 hands,
-// same box, alternating; profiles/r03_ab_staged_store.jsonl): with rest_verts
-// (two output streams) 0.600 / 0.599 ms staged (verts only) vs 0.619 / 0.612
-// plain; verts only 0.507 / 0.506 staged vs 0.495 / 0.502 plain -- so the
-// product stages the rest_verts instantiations only.
-// MANO_BS_STAGED_STORE (diagnostic builds): 0 = point stores everywhere,
-// 2 = staged everywhere, 3 = staged with rest_verts only (the product).
+// Verts leave through a per-wave LDS stage: the lanes drop their 12-B points
+// into the 16 hand rows (48 floats each), then read them back as float4 and
+// store 3 dwordx4 per lane (1 KB per instruction) instead of 4 dwordx3.
 #ifndef MANO_BS_STAGED_STORE
-#define MANO_BS_STAGED_STORE 3
+#define MANO_BS_STAGED_STORE 0
 #endif
-constexpr int kStageRow = 60;  // floats per staged hand row: [8 carry | 48 data | 4 pad]
-constexpr int kStageWaveFloats = 16 * kStageRow + 2 * 16 * 8;  // stage + two carry areas (verts, v_posed)
-
-// One output stream of one group through the stage: o[r][c] = point of hand
-// row row0 + r (vertex col); dst = the tile's first hand row; carry = the
-// stream's [16][8] carry area.  Rows past the batch end (n_valid) store the
-// last hand's identical values.  3 global stores per lane, always.
-template <bool kNt>
-__device__ __forceinline__ void store_staged(float* st, float* carry, float* dst, const float (&o)[4][3],
-                                             int row0, int col, int lane, int n_valid, int vstride32, int vb,
-                                             bool carried) {
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int c = 0; c < 3; ++c) st[(row0 + r) * kStageRow + 8 + 3 * col + c] = o[r][c];
-  // the row's carry in front of its data (c floats), and its new carry saved
-  // after the window reads below (LDS ops of one wave are in order)
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int idx = 64 * k + lane, row = idx >> 3, e = idx & 7;
-    const int hr = min(row, n_valid - 1);
-    const int c = int((reinterpret_cast<uintptr_t>(dst + unsigned(hr * vstride32)) >> 2) & 7);
-    if (carried && e < c) st[row * kStageRow + 8 - c + e] = carry[row * 8 + e];
-  }
-#pragma unroll
-  for (int m = 0; m < 3; ++m) {
-    const int i = 64 * m + lane;
-    const int hr = min(i / 12, n_valid - 1), c4 = 4 * (i % 12);
-    float* row_ptr = dst + unsigned(hr * vstride32);
-    const int c = carried ? int((reinterpret_cast<uintptr_t>(row_ptr) >> 2) & 7) : 0;
-    const float* sp = st + hr * kStageRow + 8 - c + c4;
-    const f32x4 v = f32x4{sp[0], sp[1], sp[2], sp[3]};
-    f32x4u* d = reinterpret_cast<f32x4u*>(row_ptr + unsigned(3 * vb - c + c4));
-    if constexpr (kNt) __builtin_nontemporal_store(v, d);
-    else *d = v;
-  }
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int idx = 64 * k + lane, row = idx >> 3, e = idx & 7;
-    const int hr = min(row, n_valid - 1);
-    const int c = int((reinterpret_cast<uintptr_t>(dst + unsigned(hr * vstride32)) >> 2) & 7);
-    if (e < c) carry[row * 8 + e] = st[row * kStageRow + 8 + 48 - c + e];
-  }
-}
-
+constexpr int kStageRow = 52;  // floats per staged hand row (48 + pad: conflict-free float4 reads)
 template <bool kTrans, bool kVposed>
 __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kernel(
     const float* __restrict__ features, const float* __restrict__ transforms,
@@ -480,9 +363,8 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
   // group's first tile); ring of 3.
   constexpr int kRingF4 = (kGroups16 + 1) * 64;
   constexpr int kSlots = 3;
-  constexpr bool kStaged = MANO_BS_STAGED_STORE == 2 || (MANO_BS_STAGED_STORE == 3 && kVposed);
-  constexpr int kStreamStores = kStaged ? 3 : 4;  // per output stream and group: dwordx4 / dwordx3
-  constexpr int kStores = (MANO_BS_ABLATE & 1) ? 0 : kStreamStores * (kVposed ? 2 : 1);
+  constexpr int kVertStores = MANO_BS_STAGED_STORE ? 3 : 4;  // verts stores per group (dwordx4 / dwordx3)
+  constexpr int kStores = (MANO_BS_ABLATE & 1) ? 0 : kVertStores + (kVposed ? 4 : 0);
   // vmcnt of the barrier after tile t: the wave's memory ops issued after tile
   // t + 1's DMA -- tile t + 2's DMA (at least 2 pieces per wave) and, after a
   // group's first tile, the previous group's stores.
@@ -491,7 +373,7 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
   // (the verts stage, when used, sits behind the ring in the same array: a
   // second LDS array makes hipcc wait vmcnt(0) -- the ring's DMA -- before
   // the group loop's LDS reads)
-  constexpr int kStageF4 = kStaged ? kStageWaveFloats / 4 : 0;  // per wave
+  constexpr int kStageF4 = MANO_BS_STAGED_STORE ? 16 * kStageRow / 4 : 0;  // per wave
   __shared__ f32x4 lds[kSlots * kRingF4 + 4 * kStageF4];
   __shared__ float trs[4][16 * 3];  // the wave's 16 translations, read back at the stores
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -624,25 +506,35 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
         continue;
       }
       prio_up<kStorePrio>();
-      if constexpr (kStaged) {
+      if constexpr (MANO_BS_STAGED_STORE) {
+        // Rows into the stage, then 3 float4 per lane: float4 i of the
+        // wave's 192 is row (64 m + lane) / 12, column 4 ((64 m + lane) % 12).
         float* st = reinterpret_cast<float*>(lds + kSlots * kRingF4 + wave * kStageF4);
-        const bool carried = grp > g0 && grp + 1 < n_groups;  // inside a range, not the shifted last group
-        float o[4][3];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int ht = min(row0 + r, n_valid - 1);
-#pragma unroll
-          for (int c = 0; c < 3; ++c) o[r][c] = kTrans ? out[c][r] + trs[wave][ht * 3 + c] : out[c][r];
+          const int hr = row0 + r;
+          float o0 = out[0][r], o1 = out[1][r], o2 = out[2][r];
+          if constexpr (kTrans) {
+            const int ht = min(hr, n_valid - 1);
+            o0 += trs[wave][ht * 3 + 0];
+            o1 += trs[wave][ht * 3 + 1];
+            o2 += trs[wave][ht * 3 + 2];
+          }
+          st[hr * kStageRow + 3 * col + 0] = o0;
+          st[hr * kStageRow + 3 * col + 1] = o1;
+          st[hr * kStageRow + 3 * col + 2] = o2;
+          if constexpr (kVposed)
+            store_out<false>(ptile + unsigned(min(hr, n_valid - 1) * vstride32 + voff),
+                             f32x3{p[0][r], p[1][r], p[2][r]});
         }
-        store_staged<MANO_BS_NT_STORE && !kVposed>(st, st + 16 * kStageRow, vtile, o, row0, col, lane, n_valid,
-                                                   vstride32, vb, carried);
-        if constexpr (kVposed) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int c = 0; c < 3; ++c) o[r][c] = p[c][r];
-          store_staged<false>(st, st + 16 * kStageRow + 128, ptile, o, row0, col, lane, n_valid, vstride32, vb,
-                              carried);
+        for (int m = 0; m < 3; ++m) {
+          const int i = 64 * m + lane;
+          const int hr = min(i / 12, n_valid - 1), c4 = 4 * (i % 12);  // rows past the batch: the last hand again
+          const f32x4 v = *reinterpret_cast<const f32x4*>(st + hr * kStageRow + c4);
+          float* dst = vtile + unsigned(hr * vstride32 + 3 * vb + c4);
+          if constexpr (MANO_BS_NT_STORE && !kVposed) __builtin_nontemporal_store(v, reinterpret_cast<f32x4u*>(dst));
+          else *reinterpret_cast<f32x4u*>(dst) = v;
         }
       } else {
       // One 12-B point store per row; rows past the batch end rewrite the
