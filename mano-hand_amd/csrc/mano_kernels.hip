@@ -343,14 +343,6 @@ __device__ __forceinline__ void bs_stamp(int slot, unsigned long long v) {
 }
 #endif
 
-// Diagnostic builds: 1 = each group's third basis tile is LDS-DMA-staged
-// right after the barrier that frees its slot (the end of the previous group,
-// before that group's LBS and stores) instead of at the group's start, so the
-// previous group's stores are ordered after it and get three tiles, not two,
-// to retire before a barrier's vmcnt must count them.
-#ifndef MANO_BS_EARLY_DMA
-#define MANO_BS_EARLY_DMA 0
-#endif
 #ifndef MANO_BS_BLOCKS_PER_CU
 #define MANO_BS_BLOCKS_PER_CU 3  // resident blocks per CU (diagnostic builds: 1, 2, 4)
 #endif
@@ -473,11 +465,9 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
       const bool more = grp + 1 < g1;
       f32x4 p[3];
       // Tile 3 grp + q in slot q; tile 3 grp + q + 2 goes to slot (q + 2) % 3.
-      if (!MANO_BS_EARLY_DMA || grp == g0) {
-        prio_up<kDmaPrio>();
-        if constexpr (!(MANO_BS_ABLATE & 16)) stage_basis_tile16(basis16, 3 * grp + 2, lds + 2 * kRingF4, wave, lane);
-        prio_down<kDmaPrio>();
-      }
+      prio_up<kDmaPrio>();
+      if constexpr (!(MANO_BS_ABLATE & 16)) stage_basis_tile16(basis16, 3 * grp + 2, lds + 2 * kRingF4, wave, lane);
+      prio_down<kDmaPrio>();
       const f32x4 wf = lds[kGroups16 * 64 + lane];  // read before slot 0 is re-staged
       p[0] = mfma16_tile(a, lds, lane);
       if (grp == g0) bs_barrier<kPieces>();
@@ -489,13 +479,8 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
         prio_down<kDmaPrio>();
       }
       p[1] = mfma16_tile(a, lds + kRingF4, lane);
-      if (MANO_BS_EARLY_DMA && grp > g0) {  // the previous group's stores came after this tile's DMA
-        if (more) bs_barrier<kPieces + kStores>();
-        else bs_barrier<kStores>();
-      } else {
-        if (more) bs_barrier<kPieces>();
-        else bs_barrier<0>();
-      }
+      if (more) bs_barrier<kPieces>();
+      else bs_barrier<0>();
       if (more) {
         prio_up<kDmaPrio>();
         if constexpr (!(MANO_BS_ABLATE & 16)) stage_basis_tile16(basis16, 3 * grp + 4, lds + kRingF4, wave, lane);
@@ -504,11 +489,6 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
       p[2] = mfma16_tile(a, lds + 2 * kRingF4, lane);
       if (more) bs_barrier<kPieces>();
       else bs_barrier<0>();
-      if (MANO_BS_EARLY_DMA && more) {  // the next group's third tile: slot 2 is free now
-        prio_up<kDmaPrio>();
-        if constexpr (!(MANO_BS_ABLATE & 16)) stage_basis_tile16(basis16, 3 * grp + 5, lds + 2 * kRingF4, wave, lane);
-        prio_down<kDmaPrio>();
-      }
       int vb = grp * 16;
       if (vb > n_verts - 16) vb = n_verts - 16;
       const int voff = 3 * (vb + col);
