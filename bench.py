@@ -103,6 +103,8 @@ def parse(argv=None):
     ap.add_argument("--no-check", action="store_true",
                     help="skip the correctness leg (sampled hands of the timed step vs the oracle)")
     ap.add_argument("--no-extra", action="store_true", help="skip the untimed other-path kernel table")
+    ap.add_argument("--no-dropin", action="store_true",
+                    help="skip the drop-in latency leg (MANOModel.set_params, batch 1, after timing)")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                     help="committed rocprofv3 --pmc summary: roofline.traffic when the live passes fail")
     ap.add_argument("--no-live-pmc", action="store_true",
@@ -157,6 +159,30 @@ def cpu_baseline(procs, seconds):
                         "sample": f"{bt['hands']} hands in 256-hand float64 BLAS-GEMM batches "
                                   f"(oracle/cpu_baseline.py forward_gemm) in {procs} processes x "
                                   f"{bt['seconds']:.1f} s, OMP_NUM_THREADS=1"}}
+
+
+def dropin_latency(params, device, calls=300, warmup=30, seed=7):
+    """The drop-in's batch-1 call (MANOModel.set_params(pose_abs, shape): host
+    float64 in, H2D, the two forward kernels, D2H, float64 attributes out) --
+    config C1's operation on the GPU, timed per call on the host clock."""
+    from mano_amd import MANOModel
+    m = MANOModel.from_params(params, device=device)
+    rng = np.random.default_rng(seed)
+    poses = rng.normal(0.0, 0.5, (calls + warmup, 16, 3))
+    shapes = rng.normal(0.0, 1.0, (calls + warmup, 10))
+    for i in range(warmup):
+        m.set_params(pose_abs=poses[i], shape=shapes[i])
+    ts = []
+    for i in range(warmup, warmup + calls):
+        t0 = time.perf_counter()
+        m.set_params(pose_abs=poses[i], shape=shapes[i])
+        ts.append(time.perf_counter() - t0)
+    m.engine.close()
+    ts = np.sort(np.asarray(ts)) * 1e6
+    return {"op": "MANOModel.set_params(pose_abs=(16,3), shape=(10,)) -> verts (778,3) float64, "
+                  "with J, R, rest_verts, joints updated (mano_np.py:48-115)",
+            "us_per_call_median": float(np.median(ts)), "us_per_call_p90": float(ts[int(0.9 * len(ts))]),
+            "us_per_call_mean": float(ts.mean()), "calls": calls}
 
 
 def sample_indices(B, n_random=48, seed=0):
@@ -691,8 +717,15 @@ def main(argv=None):
         }
         if gather_check is not None:
             line["gather_check"] = gather_check
+        if world == 1 and not args.no_dropin:
+            line["dropin"] = dropin_latency(params, local_dev)
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(args.cpu_procs or cpu_share(), args.cpu_seconds)
+            cb = line["cpu_baseline"]
+            if "dropin" in line and cb.get("value"):
+                # the per-hand port's time per hand on ONE core (the reference's
+                # own loop runs at 1/1.055 of it: profiles/cpu_calibration.json)
+                line["dropin"]["cpu_port_us_per_hand_one_core"] = cb["cores"] / cb["value"] * 1e6
         print(json.dumps(line), flush=True)
     if gatherer is not None:
         gatherer.close()

@@ -437,6 +437,7 @@ class MANOModel:
         self.J = None
         self.R = None
         self.joints = None
+        self._io = None
         self.update()
 
     def _dev(self, a) -> torch.Tensor:
@@ -474,6 +475,33 @@ class MANOModel:
         self.update()
         return self.verts.copy()
 
+    # The batch-1 update's inputs and outputs, packed: one pinned host block
+    # and one device block each way, so a call is one H2D copy, the two
+    # forward kernels, one D2H copy and one stream sync.
+    _IN = (("shape", (1, N_SHAPE)), ("pose", (1, N_JOINTS, 3)), ("trans", (1, 3)))
+
+    def _io_buffers(self):
+        if self._io is None:
+            V = self.engine.n_verts
+            outs = (("verts", (1, V, 3)), ("joints", (1, N_JOINTS, 3)), ("rest_verts", (1, V, 3)),
+                    ("rest_joints", (1, N_JOINTS, 3)), ("rot_mats", (1, N_JOINTS, 3, 3)))
+
+            def carve(spec, dev, pinned):
+                n = sum(int(np.prod(shp)) for _, shp in spec)
+                d = torch.empty(n, dtype=torch.float32, device=dev)
+                h = torch.empty(n, dtype=torch.float32, pin_memory=pinned)
+                views, o = {}, 0
+                for name, shp in spec:
+                    k = int(np.prod(shp))
+                    views[name] = (d[o:o + k].view(shp), h[o:o + k].numpy().reshape(shp[1:]))
+                    o += k
+                return d, h, views
+
+            d_in, h_in, v_in = carve(self._IN, self.device, True)
+            d_out, h_out, v_out = carve(outs, self.device, True)
+            self._io = (d_in, h_in, v_in, d_out, h_out, v_out)
+        return self._io
+
     def update(self):
         """Recompute every output on the GPU from pose / shape (mano_np.py:79-115)."""
         pose = np.asarray(self.pose.reshape((-1, 1, 3)), dtype=np.float64)  # list -> AttributeError
@@ -482,10 +510,19 @@ class MANOModel:
         shape = np.asarray(self.shape, dtype=np.float64)
         if shape.shape != (self.n_shape_params,):
             raise ValueError(f"shape has shape {shape.shape}, ({self.n_shape_params},) expected")
-        trans = None if not np.any(self.trans) else self._dev(self.trans)[None]
-        out = self.engine.forward(self._dev(shape)[None], self._dev(pose.reshape(1, self.n_joints, 3)),
-                                  trans, joints=True, rest_verts=True, rest_joints=True, rot_mats=True)
-        host = {k: v[0].double().cpu().numpy() for k, v in out.items()}
+        d_in, h_in, v_in, d_out, h_out, v_out = self._io_buffers()
+        # float64 -> float32 exactly as np.asarray(..., dtype=np.float32) would
+        v_in["shape"][1][...] = shape
+        v_in["pose"][1][...] = pose.reshape(self.n_joints, 3)
+        v_in["trans"][1][...] = self.trans
+        s = torch.cuda.current_stream(self.device)
+        d_in.copy_(h_in, non_blocking=True)
+        self.engine.forward(v_in["shape"][0], v_in["pose"][0], v_in["trans"][0] if np.any(self.trans) else None,
+                            joints=True, rest_verts=True, rest_joints=True, rot_mats=True,
+                            out={k: dv for k, (dv, _) in v_out.items()})
+        h_out.copy_(d_out, non_blocking=True)
+        s.synchronize()
+        host = {k: hv.astype(np.float64) for k, (_, hv) in v_out.items()}
         self.verts = host["verts"]
         self.rest_verts = host["rest_verts"]
         self.J = host["rest_joints"]

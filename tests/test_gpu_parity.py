@@ -336,6 +336,34 @@ def test_dropin_quirks(params):
     assert np.abs(m.joints - j0 - [0.1, -0.2, 0.3]).max() < 1e-6
 
 
+def test_dropin_packed_io_matches_batched(engine, dev, params):
+    """The drop-in's packed batch-1 I/O (one H2D, one D2H through pinned
+    buffers) returns the batched engine's bits, and its results are owned
+    copies: a later call changes neither an earlier return nor its attributes."""
+    from mano_amd import MANOModel
+    m = MANOModel.from_params(params, device=0)
+    rng = np.random.default_rng(5)
+    pose_a, pose_b = rng.normal(0, 0.5, (2, 16, 3))
+    beta_a, beta_b = rng.normal(0, 1, (2, 10))
+    va = m.set_params(pose_abs=pose_a, shape=beta_a, trans=[0.01, 0.02, -0.03])
+    keep = {k: getattr(m, k) for k in ("verts", "rest_verts", "J", "R", "joints")}
+    snap = {k: v.copy() for k, v in keep.items()}
+    va_copy = va.copy()
+    m.set_params(pose_abs=pose_b, shape=beta_b)
+    assert np.array_equal(va, va_copy)
+    for k in keep:
+        assert np.array_equal(keep[k], snap[k]), k
+    out = engine.forward(torch.tensor(beta_a, dtype=torch.float32, device=dev)[None],
+                         torch.tensor(pose_a, dtype=torch.float32, device=dev)[None],
+                         torch.tensor([[0.01, 0.02, -0.03]], dtype=torch.float32, device=dev),
+                         joints=True, rest_verts=True, rest_joints=True, rot_mats=True)
+    want = {"verts": "verts", "rest_verts": "rest_verts", "J": "rest_joints", "R": "rot_mats",
+            "joints": "joints"}
+    for k, o in want.items():
+        assert snap[k].dtype == np.float64
+        assert np.array_equal(snap[k], out[o][0].double().cpu().numpy()), k
+
+
 @pytest.mark.parametrize("B", [1, 33, 200, 4096])
 def test_fused_equals_unfused(engine, dev, params, B):
     """blend_skin (fused, v_posed on chip) == blend then skin, bit for bit."""

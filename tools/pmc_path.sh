@@ -24,12 +24,13 @@ for p in sys.argv[2:]:
             for r in csv.DictReader(open(f)):
                 if r["Counter_Name"] != c:
                     continue
-                k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("mano::(anonymous namespace)::", "")
+                # strip the namespace first: "(anonymous namespace)" holds a "("
+                k = r["Kernel_Name"].replace("void ", "").replace("mano::(anonymous namespace)::", "").split("(")[0]
                 acc[k][c].append(float(r["Counter_Value"]))
     res[p] = {k: {"read_bytes": 2 * 1024 * sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"]),
                   "write_bytes": 1024 * sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"]),
                   "launches": len(d["WRITE_SIZE"])}
-              for k, d in acc.items() if d["FETCH_SIZE"] and d["WRITE_SIZE"] and "mano" not in k[:4]}
+              for k, d in acc.items() if d["FETCH_SIZE"] and d["WRITE_SIZE"]}
 json.dump(res, open(f"{out}/pmc_path.json", "w"), indent=1)
 for p, ks in res.items():
     for k, v in ks.items():
