@@ -179,6 +179,12 @@ __device__ __forceinline__ void pca_joint_pose(const PcaInput& in, const float* 
   }
 }
 
+// Diagnostic builds: 1 = the X rows and transforms leave as nontemporal
+// stores (the verdict's "X-row stores made nontemporal").
+#ifndef MANO_ART_NT_STORE
+#define MANO_ART_NT_STORE 0
+#endif
+
 // kFromPca: the pose comes from PCA coefficients (pca_joint_pose prologue, the
 // basis rows in use staged in LDS) instead of the axis-angle `pose` input.
 template <bool kFromPca>
@@ -248,9 +254,15 @@ __global__ __launch_bounds__(256) void articulate_kernel(
   articulate_joint(aa[0], aa[1], aa[2], beta, j, src, depth[j], max_depth, jt_s, js_s, rm, J, t, Aj);
   if (valid) {
     f32x4* A = reinterpret_cast<f32x4*>(transforms + h * kTransformFloats + j * 12);
-    A[0] = f32x4{Aj[0], Aj[1], Aj[2], Aj[3]};
-    A[1] = f32x4{Aj[4], Aj[5], Aj[6], Aj[7]};
-    A[2] = f32x4{Aj[8], Aj[9], Aj[10], Aj[11]};
+    if constexpr (MANO_ART_NT_STORE) {
+      __builtin_nontemporal_store(f32x4{Aj[0], Aj[1], Aj[2], Aj[3]}, A + 0);
+      __builtin_nontemporal_store(f32x4{Aj[4], Aj[5], Aj[6], Aj[7]}, A + 1);
+      __builtin_nontemporal_store(f32x4{Aj[8], Aj[9], Aj[10], Aj[11]}, A + 2);
+    } else {
+      A[0] = f32x4{Aj[0], Aj[1], Aj[2], Aj[3]};
+      A[1] = f32x4{Aj[4], Aj[5], Aj[6], Aj[7]};
+      A[2] = f32x4{Aj[8], Aj[9], Aj[10], Aj[11]};
+    }
     store_joint_outputs(h, j, trans, rm, J, t, joints, rest_joints, rot_mats);
   }
 
@@ -270,7 +282,10 @@ __global__ __launch_bounds__(256) void articulate_kernel(
   __syncthreads();
   const int n_rows = int(n - h0 < 16 ? n - h0 : 16);
   f32x4* dst = reinterpret_cast<f32x4*>(features + h0 * kXStride);
-  for (int i = tid; i < n_rows * (kXStride / 4); i += 256) dst[i] = xs4[i];
+  for (int i = tid; i < n_rows * (kXStride / 4); i += 256) {
+    if constexpr (MANO_ART_NT_STORE) __builtin_nontemporal_store(xs4[i], dst + i);
+    else dst[i] = xs4[i];
+  }
 }
 
 // ---------------------------------------------------------------------------

@@ -438,6 +438,7 @@ class MANOModel:
         self.R = None
         self.joints = None
         self._io = None
+        self._graphs = {}
         self.update()
 
     def _dev(self, a) -> torch.Tensor:
@@ -477,8 +478,11 @@ class MANOModel:
 
     # The batch-1 update's inputs and outputs, packed: one pinned host block
     # and one device block each way, so a call is one H2D copy, the two
-    # forward kernels, one D2H copy and one stream sync.
+    # forward kernels, one D2H copy and one stream sync -- captured once (per
+    # with/without translation) into a HIP graph and replayed, so a call
+    # costs one graph launch instead of four.
     _IN = (("shape", (1, N_SHAPE)), ("pose", (1, N_JOINTS, 3)), ("trans", (1, 3)))
+    use_graphs = True
 
     def _io_buffers(self):
         if self._io is None:
@@ -515,12 +519,13 @@ class MANOModel:
         v_in["shape"][1][...] = shape
         v_in["pose"][1][...] = pose.reshape(self.n_joints, 3)
         v_in["trans"][1][...] = self.trans
+        with_trans = bool(np.any(self.trans))
         s = torch.cuda.current_stream(self.device)
-        d_in.copy_(h_in, non_blocking=True)
-        self.engine.forward(v_in["shape"][0], v_in["pose"][0], v_in["trans"][0] if np.any(self.trans) else None,
-                            joints=True, rest_verts=True, rest_joints=True, rot_mats=True,
-                            out={k: dv for k, (dv, _) in v_out.items()})
-        h_out.copy_(d_out, non_blocking=True)
+        g = self._graph(with_trans) if self.use_graphs else None
+        if g is not None:
+            g.replay()
+        else:
+            self._update_body(with_trans)
         s.synchronize()
         host = {k: hv.astype(np.float64) for k, (_, hv) in v_out.items()}
         self.verts = host["verts"]
@@ -528,6 +533,40 @@ class MANOModel:
         self.J = host["rest_joints"]
         self.R = host["rot_mats"]
         self.joints = host["joints"]
+
+    def _update_body(self, with_trans):
+        """H2D of the packed inputs, mano_forward, D2H of the packed outputs
+        (on the current stream; no sync)."""
+        d_in, h_in, v_in, d_out, h_out, v_out = self._io_buffers()
+        d_in.copy_(h_in, non_blocking=True)
+        self.engine.forward(v_in["shape"][0], v_in["pose"][0], v_in["trans"][0] if with_trans else None,
+                            joints=True, rest_verts=True, rest_joints=True, rot_mats=True,
+                            out={k: dv for k, (dv, _) in v_out.items()})
+        h_out.copy_(d_out, non_blocking=True)
+
+    def _graph(self, with_trans):
+        """The update body captured into a HIP graph (one per translation
+        mode), built on first use: an eager run on the capture stream first
+        (it allocates that stream's workspace outside the capture)."""
+        if with_trans not in self._graphs:
+            g = None
+            cur = torch.cuda.current_stream(self.device)
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                self._update_body(with_trans)
+            side.synchronize()
+            try:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=side):
+                    self._update_body(with_trans)
+            except RuntimeError:
+                g = None  # capture refused: keep the eager launches (same kernels)
+            cur.wait_stream(side)
+            # the graph holds raw pointers into `side`'s workspace: keep the
+            # stream (and so its workspace entry, batch 1, never regrown) alive
+            self._graphs[with_trans] = (g, side)
+        return self._graphs[with_trans][0]
 
     def forward_batch(self, betas, pose, trans=None, **kw):
         """Batched forward on device tensors; see `ManoHip.forward`."""

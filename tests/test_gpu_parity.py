@@ -336,12 +336,15 @@ def test_dropin_quirks(params):
     assert np.abs(m.joints - j0 - [0.1, -0.2, 0.3]).max() < 1e-6
 
 
-def test_dropin_packed_io_matches_batched(engine, dev, params):
+@pytest.mark.parametrize("graphs", [True, False])
+def test_dropin_packed_io_matches_batched(engine, dev, params, graphs):
     """The drop-in's packed batch-1 I/O (one H2D, one D2H through pinned
-    buffers) returns the batched engine's bits, and its results are owned
-    copies: a later call changes neither an earlier return nor its attributes."""
+    buffers; replayed from a HIP graph or launched eagerly) returns the
+    batched engine's bits, and its results are owned copies: a later call
+    changes neither an earlier return nor its attributes."""
     from mano_amd import MANOModel
     m = MANOModel.from_params(params, device=0)
+    m.use_graphs = graphs
     rng = np.random.default_rng(5)
     pose_a, pose_b = rng.normal(0, 0.5, (2, 16, 3))
     beta_a, beta_b = rng.normal(0, 1, (2, 10))
@@ -362,6 +365,11 @@ def test_dropin_packed_io_matches_batched(engine, dev, params):
     for k, o in want.items():
         assert snap[k].dtype == np.float64
         assert np.array_equal(snap[k], out[o][0].double().cpu().numpy()), k
+    if graphs:  # both translation modes captured, and replayed (not the eager fallback)
+        assert all(g is not None for g, _ in m._graphs.values()) and set(m._graphs) == {True, False}
+    # alternating modes and repeated inputs reproduce the same bits
+    again = m.set_params(pose_abs=pose_a, shape=beta_a, trans=[0.01, 0.02, -0.03])
+    assert np.array_equal(again, va_copy)
 
 
 @pytest.mark.parametrize("B", [1, 33, 200, 4096])

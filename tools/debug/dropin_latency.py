@@ -1,6 +1,7 @@
-"""Per-call latency of the drop-in MANOModel.set_params (batch 1), packed I/O
-(model.py: one pinned H2D, one D2H) vs the round-2 form (a device tensor per
-input, a .double().cpu() per output), same model, same inputs, same process.
+"""Per-call latency of the drop-in MANOModel.set_params (batch 1): packed I/O
+(model.py: one pinned H2D, one D2H) replayed from a HIP graph, the same
+launched eagerly, and the round-2 form (a device tensor per input, a
+.double().cpu() per output); same model, same inputs, same process.
 
     python tools/debug/dropin_latency.py [--calls 300]
 """
@@ -43,8 +44,10 @@ def main():
     shapes = rng.normal(0, 1, (a.calls, 10))
     res = {}
     packed = model_mod.MANOModel.update
-    for name, upd in (("packed", packed), ("per_array", per_array_update), ("packed_again", packed)):
+    for name, upd, graphs in (("graph", packed, True), ("packed", packed, False),
+                              ("per_array", per_array_update, False), ("graph_again", packed, True)):
         model_mod.MANOModel.update = upd
+        model_mod.MANOModel.use_graphs = graphs
         m = MANOModel.from_params(params, device=0)
         outs = []
         for i in range(30):
@@ -59,7 +62,8 @@ def main():
                      "digest": float(np.sum(np.stack(outs)[:, ::7]))}
         m.engine.close()
     model_mod.MANOModel.update = packed
-    res["same_results"] = res["packed"]["digest"] == res["per_array"]["digest"]
+    model_mod.MANOModel.use_graphs = True
+    res["same_results"] = len({res[k]["digest"] for k in ("graph", "packed", "per_array")}) == 1
     print(json.dumps(res))
 
 
