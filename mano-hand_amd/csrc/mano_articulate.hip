@@ -179,12 +179,6 @@ __device__ __forceinline__ void pca_joint_pose(const PcaInput& in, const float* 
   }
 }
 
-// Diagnostic builds: 1 = the X rows and transforms leave as nontemporal
-// stores (the verdict's "X-row stores made nontemporal").
-#ifndef MANO_ART_NT_STORE
-#define MANO_ART_NT_STORE 0
-#endif
-
 // kFromPca: the pose comes from PCA coefficients (pca_joint_pose prologue, the
 // basis rows in use staged in LDS) instead of the axis-angle `pose` input.
 template <bool kFromPca>
@@ -197,6 +191,10 @@ __global__ __launch_bounds__(256) void articulate_kernel(
     float* __restrict__ rest_joints, float* __restrict__ rot_mats, PcaInput pca,
     const float* __restrict__ pca_basis, const float* __restrict__ pca_mean) {
   __shared__ f32x4 xs4[16 * kXStride / 4];
+  // The block's 16 rows of posed joints (48 floats each), staged so they
+  // leave as one contiguous dwordx4 stream like the X rows (three 4-B
+  // stores per lane at a 12-B stride cost the in-path step ~7 us).
+  __shared__ f32x4 jo4[16 * kJoints * 3 / 4];
   // The folded joint regressor (J = Jt + Js . beta, 528 floats), staged once
   // per block: each lane reads its joint's 33 values from LDS, not HBM/L2.
   __shared__ float jt_s[kJoints * 3];
@@ -208,6 +206,8 @@ __global__ __launch_bounds__(256) void articulate_kernel(
   const int64_t h0 = int64_t(blockIdx.x) * 16;
   const int64_t h = min(h0 + hl, n - 1);  // tail lanes repeat the last hand
   const bool valid = h0 + hl < n;
+  // a caller's joints buffer that is not 16-B aligned takes the per-lane stores
+  const bool joints_direct = (reinterpret_cast<uintptr_t>(joints) & 15) != 0;
 
   // Every global load of the prologue is issued before the first LDS write
   // (the lane's pose and betas, then the block's regressor fold): written as
@@ -254,16 +254,15 @@ __global__ __launch_bounds__(256) void articulate_kernel(
   articulate_joint(aa[0], aa[1], aa[2], beta, j, src, depth[j], max_depth, jt_s, js_s, rm, J, t, Aj);
   if (valid) {
     f32x4* A = reinterpret_cast<f32x4*>(transforms + h * kTransformFloats + j * 12);
-    if constexpr (MANO_ART_NT_STORE) {
-      __builtin_nontemporal_store(f32x4{Aj[0], Aj[1], Aj[2], Aj[3]}, A + 0);
-      __builtin_nontemporal_store(f32x4{Aj[4], Aj[5], Aj[6], Aj[7]}, A + 1);
-      __builtin_nontemporal_store(f32x4{Aj[8], Aj[9], Aj[10], Aj[11]}, A + 2);
-    } else {
-      A[0] = f32x4{Aj[0], Aj[1], Aj[2], Aj[3]};
-      A[1] = f32x4{Aj[4], Aj[5], Aj[6], Aj[7]};
-      A[2] = f32x4{Aj[8], Aj[9], Aj[10], Aj[11]};
-    }
-    store_joint_outputs(h, j, trans, rm, J, t, joints, rest_joints, rot_mats);
+    A[0] = f32x4{Aj[0], Aj[1], Aj[2], Aj[3]};
+    A[1] = f32x4{Aj[4], Aj[5], Aj[6], Aj[7]};
+    A[2] = f32x4{Aj[8], Aj[9], Aj[10], Aj[11]};
+    store_joint_outputs(h, j, trans, rm, J, t, joints_direct ? joints : nullptr, rest_joints, rot_mats);
+  }
+  if (joints && !joints_direct) {
+    float* o = reinterpret_cast<float*>(jo4) + hl * (kJoints * 3) + 3 * j;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) o[c] = t[c] + (trans ? trans[h * 3 + c] : 0.f);
   }
 
   // Row of X: k < 10 beta, 10 <= k < 145 features (k = 10 + 9(j-1) + 3 row +
@@ -281,11 +280,12 @@ __global__ __launch_bounds__(256) void articulate_kernel(
   }
   __syncthreads();
   const int n_rows = int(n - h0 < 16 ? n - h0 : 16);
-  f32x4* dst = reinterpret_cast<f32x4*>(features + h0 * kXStride);
-  for (int i = tid; i < n_rows * (kXStride / 4); i += 256) {
-    if constexpr (MANO_ART_NT_STORE) __builtin_nontemporal_store(xs4[i], dst + i);
-    else dst[i] = xs4[i];
+  if (joints && !joints_direct) {
+    f32x4* jd = reinterpret_cast<f32x4*>(joints + h0 * (kJoints * 3));
+    for (int i = tid; i < n_rows * (kJoints * 3 / 4); i += 256) jd[i] = jo4[i];
   }
+  f32x4* dst = reinterpret_cast<f32x4*>(features + h0 * kXStride);
+  for (int i = tid; i < n_rows * (kXStride / 4); i += 256) dst[i] = xs4[i];
 }
 
 // ---------------------------------------------------------------------------

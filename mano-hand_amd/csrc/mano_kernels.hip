@@ -887,14 +887,20 @@ int64_t resident_blocks(Kernel kernel, const DeviceModel& m, int design_per_cu) 
 }
 
 // At least this many (tile, group) units per worker: below it, splitting a
-// tile's groups over more workers costs more operand set-up than it gains.
+// tile's groups over more workers costs more operand set-up than it gains --
+// except while that would leave CUs empty: small launches (the drop-in's
+// batch of 1 is 49 units) spread one block per CU, down to a unit per worker,
+// for latency.
 constexpr int64_t kMinUnitsPerWorker = 8;
 
 template <class Kernel>
 dim3 persistent_grid(Kernel kernel, const DeviceModel& m, int64_t units, int workers_per_block,
                      int design_per_cu) {
   const int64_t want = (units + kMinUnitsPerWorker - 1) / kMinUnitsPerWorker;
-  const int64_t blocks_wanted = (want + workers_per_block - 1) / workers_per_block;
+  int64_t blocks_wanted = (want + workers_per_block - 1) / workers_per_block;
+  const int64_t spread = (units + workers_per_block - 1) / workers_per_block;
+  const int64_t n_cu = m.n_cu > 0 ? m.n_cu : 1;
+  if (blocks_wanted < n_cu) blocks_wanted = spread < n_cu ? spread : n_cu;
   const int64_t cap = resident_blocks(kernel, m, design_per_cu);
   return dim3{unsigned(blocks_wanted < cap ? blocks_wanted : cap)};
 }

@@ -158,6 +158,31 @@ def test_shared_betas_stride_zero(engine, dev, params):
     assert np.abs(host(out["verts"]) - ref["verts"]).max() <= TOL_M
 
 
+@pytest.mark.parametrize("B", [1, 15, 16, 17, 300])
+def test_joints_staged_and_unaligned(engine, dev, params, B):
+    """Posed joints leave articulate as a staged dwordx4 stream when the
+    caller's buffer is 16-B aligned, per lane otherwise: same bits both
+    ways, with and without trans, and nothing written past row B."""
+    rng = np.random.default_rng(40 + B)
+    beta = f32(rng.normal(0, 1, (B, 10)), dev)
+    pose = f32(rng.normal(0, 0.5, (B, 16, 3)), dev)
+    trans = f32(rng.uniform(-1, 1, (B, 3)), dev)
+    for tr in (None, trans):
+        a = engine.forward(beta, pose, tr, joints=True)["joints"]
+        raw = torch.full((B * 48 + 8,), 7.0, device=dev)
+        ju = raw[1:1 + B * 48].view(B, 16, 3)  # 4-B offset: per-lane stores
+        engine.forward(beta, pose, tr, joints=True, out={"joints": ju})
+        assert torch.equal(a, ju)
+        assert raw[0].item() == 7.0 and torch.all(raw[1 + B * 48:] == 7.0)
+        raw.fill_(7.0)
+        ja = raw[4:4 + B * 48].view(B, 16, 3)  # 16-B offset: the staged stream
+        engine.forward(beta, pose, tr, joints=True, out={"joints": ja})
+        assert torch.equal(a, ja)
+        assert torch.all(raw[:4] == 7.0) and torch.all(raw[4 + B * 48:] == 7.0)
+    ref = mano_oracle.forward(params, host(beta), host(pose), host(trans))
+    assert np.abs(host(a) - ref["joints"]).max() <= TOL_M
+
+
 def test_flat48_pose(engine, dev, params):
     rng = np.random.default_rng(5)
     pose = rng.normal(0, 0.5, (20, 48))

@@ -64,6 +64,9 @@ res["fused"] = {"articulate": a, "blend_skin": f, "step": a + f}
 res["fused_digest"] = digest(v)
 res["blend_skin_rest_verts"] = steps([lambda: m.stage_blend_skin(B, v, rest_verts=vp)])[0]
 jo = torch.empty((B, 16, 3), device="cuda:0")
+# bench.py's forward step: the articulation also writes the posed joints
+a, f = steps([lambda: m.stage_articulate(betas, pose, joints=jo), lambda: m.stage_blend_skin(B, v)])
+res["fused_joints"] = {"articulate": a, "blend_skin": f, "step": a + f}
 outd = {"verts": v, "joints": jo}
 res["single_launch"] = steps([lambda: m.forward(betas, pose, None, joints=True, out=outd)])[0]
 res["single_digest"] = [digest(v), digest(jo)]

@@ -22,5 +22,5 @@ if [ -z "${SKIP_TESTS:-}" ]; then
 fi
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 400 python bench.py --steps 20 --warmup 5
-step stats 400 rocprofv3 --kernel-trace --stats -d $OUT/stats -o bench --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu --no-live-pmc
+step stats 400 rocprofv3 --kernel-trace --stats -d $OUT/stats -o bench --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu --no-live-pmc --no-dropin
 if [ -n "${EXTRA:-}" ]; then step extra 600 bash -c "$EXTRA"; fi
