@@ -521,7 +521,8 @@ class MANOModel:
         v_in["trans"][1][...] = self.trans
         with_trans = bool(np.any(self.trans))
         s = torch.cuda.current_stream(self.device)
-        g = self._graph(with_trans) if self.use_graphs else None
+        # a graph replays the kernels of the precision it was captured with
+        g = self._graph((with_trans, self.engine.precision)) if self.use_graphs else None
         if g is not None:
             g.replay()
         else:
@@ -544,11 +545,13 @@ class MANOModel:
                             out={k: dv for k, (dv, _) in v_out.items()})
         h_out.copy_(d_out, non_blocking=True)
 
-    def _graph(self, with_trans):
+    def _graph(self, key):
         """The update body captured into a HIP graph (one per translation
-        mode), built on first use: an eager run on the capture stream first
-        (it allocates that stream's workspace outside the capture)."""
-        if with_trans not in self._graphs:
+        mode and engine precision), built on first use: an eager run on the
+        capture stream first (it allocates that stream's workspace outside the
+        capture)."""
+        with_trans = key[0]
+        if key not in self._graphs:
             g = None
             cur = torch.cuda.current_stream(self.device)
             side = torch.cuda.Stream(self.device)
@@ -565,8 +568,8 @@ class MANOModel:
             cur.wait_stream(side)
             # the graph holds raw pointers into `side`'s workspace: keep the
             # stream (and so its workspace entry, batch 1, never regrown) alive
-            self._graphs[with_trans] = (g, side)
-        return self._graphs[with_trans][0]
+            self._graphs[key] = (g, side)
+        return self._graphs[key][0]
 
     def forward_batch(self, betas, pose, trans=None, **kw):
         """Batched forward on device tensors; see `ManoHip.forward`."""

@@ -391,10 +391,19 @@ def test_dropin_packed_io_matches_batched(engine, dev, params, graphs):
         assert snap[k].dtype == np.float64
         assert np.array_equal(snap[k], out[o][0].double().cpu().numpy()), k
     if graphs:  # both translation modes captured, and replayed (not the eager fallback)
-        assert all(g is not None for g, _ in m._graphs.values()) and set(m._graphs) == {True, False}
+        assert all(g is not None for g, _ in m._graphs.values())
+        assert set(m._graphs) == {(True, "fp32"), (False, "fp32")}
     # alternating modes and repeated inputs reproduce the same bits
     again = m.set_params(pose_abs=pose_a, shape=beta_a, trans=[0.01, 0.02, -0.03])
     assert np.array_equal(again, va_copy)
+    # a precision switch is honoured (its own graph), and switching back reproduces the fp32 bits
+    m.engine.set_precision("f16x3")
+    h3 = m.set_params(pose_abs=pose_a, shape=beta_a)
+    ref = engine.forward(torch.tensor(beta_a, dtype=torch.float32, device=dev)[None],
+                         torch.tensor(pose_a, dtype=torch.float32, device=dev)[None])["verts"][0]
+    assert np.abs(h3 - ref.double().cpu().numpy()).max() <= TOL_M
+    m.engine.set_precision("fp32")
+    assert np.array_equal(m.set_params(pose_abs=pose_a, shape=beta_a, trans=[0.01, 0.02, -0.03]), va_copy)
 
 
 @pytest.mark.parametrize("B", [1, 33, 200, 4096])
