@@ -315,6 +315,15 @@ def pmc_values(d, counter, name_fragment):
     return vals
 
 
+def pmc_child_args(args, batch):
+    """bench.py arguments of the --pmc child: the timed path's launches only
+    (no drop-in leg, whose batch-1 launches of the same kernel would dilute
+    the per-launch average; no correctness, CPU or extra-table legs)."""
+    return ["--workload", args.workload, "--batch", str(batch), "--precision", args.precision,
+            "--path", args.path, "--steps", "3", "--warmup", "1", "--ramp-seconds", "0",
+            "--no-cpu", "--no-extra", "--no-live-pmc", "--no-check", "--no-dropin"]
+
+
 def live_traffic(args, batch, name_fragment, timeout=120):
     """HBM bytes per launch of the dominant kernel measured in this run: rocprofv3
     --pmc FETCH_SIZE and --pmc WRITE_SIZE as two separate passes (the counter
@@ -330,9 +339,7 @@ def live_traffic(args, batch, name_fragment, timeout=120):
     rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(rp):
         return None, "rocprofv3 not found"
-    child = [sys.executable, os.path.abspath(__file__), "--workload", args.workload, "--batch", str(batch),
-             "--precision", args.precision, "--path", args.path, "--steps", "3", "--warmup", "1",
-             "--ramp-seconds", "0", "--no-cpu", "--no-extra", "--no-live-pmc", "--no-check"]
+    child = [sys.executable, os.path.abspath(__file__), *pmc_child_args(args, batch)]
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK",
                         "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}

@@ -115,3 +115,14 @@ def test_sample_indices_cover_edges():
     for h in (0, 15, 16, 63, 64, 32767, 32768, 65535):
         assert h in idx
     assert bench.sample_indices(3).tolist() == [0, 1, 2]
+
+
+def test_pmc_child_measures_the_timed_path_only():
+    """The --pmc child must not run the drop-in leg: its batch-1 launches of
+    the same kernel would dilute roofline.traffic's per-launch average (round
+    3 lines r03g-r03i read 36 MB for 857 MB launches)."""
+    args = bench.parse(["--workload", "C2"])
+    child = bench.pmc_child_args(args, 65536)
+    assert "--no-dropin" in child and "--no-check" in child and "--no-live-pmc" in child
+    parsed = bench.parse(child)
+    assert parsed.no_dropin and parsed.batch == 65536 and parsed.path == args.path
