@@ -398,7 +398,7 @@ def test_dropin_packed_io_matches_batched(engine, dev, params, graphs):
     assert np.array_equal(again, va_copy)
     # a precision switch is honoured (its own graph), and switching back reproduces the fp32 bits
     m.engine.set_precision("f16x3")
-    h3 = m.set_params(pose_abs=pose_a, shape=beta_a)
+    h3 = m.set_params(pose_abs=pose_a, shape=beta_a, trans=[0.0, 0.0, 0.0])  # trans is kept across calls
     ref = engine.forward(torch.tensor(beta_a, dtype=torch.float32, device=dev)[None],
                          torch.tensor(pose_a, dtype=torch.float32, device=dev)[None])["verts"][0]
     assert np.abs(h3 - ref.double().cpu().numpy()).max() <= TOL_M
