@@ -307,8 +307,8 @@ __device__ __forceinline__ void bs_barrier() {
 // 0.493 vs 0.504 ms, identical bits).  With rest_verts as a second stream
 // they are plain: nontemporal there took 0.85 vs 0.61 ms, and the unfused
 // blend GEMM (0.60 vs 0.37) and blend_skin_h3 (0.40 vs 0.26) lose the same way.
-// (Diagnostic builds: 2 = verts nontemporal beside plain rest_verts, 3 = the
-// reverse.)
+// Either stream alone nontemporal beside the other plain is as bad (0.72-0.74
+// vs 0.62 ms, profiles/r03k_ab_nt_rest_verts.jsonl).
 #ifndef MANO_BS_NT_STORE
 #define MANO_BS_NT_STORE 1
 #endif
@@ -553,9 +553,9 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
         if constexpr (MANO_BS_ABLATE == 4)  // needs a verts buffer of n * 49 * 256 B
           *reinterpret_cast<f32x3*>(verts + ((h0 + hr) * n_groups + grp) * 64 + 3 * col) = f32x3{o0, o1, o2};
         else
-          store_out<(MANO_BS_NT_STORE && !kVposed) || MANO_BS_NT_STORE == 2>(vtile + unsigned(hr * vstride32 + voff), f32x3{o0, o1, o2});
+          store_out<MANO_BS_NT_STORE && !kVposed>(vtile + unsigned(hr * vstride32 + voff), f32x3{o0, o1, o2});
         if constexpr (kVposed)
-          store_out<MANO_BS_NT_STORE == 3>(ptile + unsigned(hr * vstride32 + voff), f32x3{p[0][r], p[1][r], p[2][r]});
+          store_out<false>(ptile + unsigned(hr * vstride32 + voff), f32x3{p[0][r], p[1][r], p[2][r]});
       }
       }
       prio_down<kStorePrio>();
