@@ -348,13 +348,6 @@ __device__ __forceinline__ void bs_stamp(int slot, unsigned long long v) {
 #ifndef MANO_BS_BLOCKS_PER_CU
 #define MANO_BS_BLOCKS_PER_CU 3  // resident blocks per CU (diagnostic builds: 1, 2, 4)
 #endif
-// Verts leave through a per-wave LDS stage: the lanes drop their 12-B points
-// into the 16 hand rows (48 floats each), then read them back as float4 and
-// store 3 dwordx4 per lane (1 KB per instruction) instead of 4 dwordx3.
-#ifndef MANO_BS_STAGED_STORE
-#define MANO_BS_STAGED_STORE 0
-#endif
-constexpr int kStageRow = 52;  // floats per staged hand row (48 + pad: conflict-free float4 reads)
 template <bool kTrans, bool kVposed>
 __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kernel(
     const float* __restrict__ features, const float* __restrict__ transforms,
@@ -365,18 +358,13 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
   // group's first tile); ring of 3.
   constexpr int kRingF4 = (kGroups16 + 1) * 64;
   constexpr int kSlots = 3;
-  constexpr int kVertStores = MANO_BS_STAGED_STORE ? 3 : 4;  // verts stores per group (dwordx4 / dwordx3)
-  constexpr int kStores = (MANO_BS_ABLATE & 1) ? 0 : kVertStores + (kVposed ? 4 : 0);
+  constexpr int kStores = (MANO_BS_ABLATE & 1) ? 0 : (kVposed ? 8 : 4);  // dwordx3 point stores per group
   // vmcnt of the barrier after tile t: the wave's memory ops issued after tile
   // t + 1's DMA -- tile t + 2's DMA (at least 2 pieces per wave) and, after a
   // group's first tile, the previous group's stores.
   constexpr int kPieces = kGroups16 / 4;     // LDS-DMA pieces per wave and tile, at least
   constexpr int kDmaPrio = MANO_BS_DMA_PRIO, kStorePrio = MANO_BS_STORE_PRIO;
-  // (the verts stage, when used, sits behind the ring in the same array: a
-  // second LDS array makes hipcc wait vmcnt(0) -- the ring's DMA -- before
-  // the group loop's LDS reads)
-  constexpr int kStageF4 = MANO_BS_STAGED_STORE ? 16 * kStageRow / 4 : 0;  // per wave
-  __shared__ f32x4 lds[kSlots * kRingF4 + 4 * kStageF4];
+  __shared__ f32x4 lds[kSlots * kRingF4];
   __shared__ float trs[4][16 * 3];  // the wave's 16 translations, read back at the stores
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int vstride32 = 3 * n_verts;
@@ -508,37 +496,6 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
         continue;
       }
       prio_up<kStorePrio>();
-      if constexpr (MANO_BS_STAGED_STORE) {
-        // Rows into the stage, then 3 float4 per lane: float4 i of the
-        // wave's 192 is row (64 m + lane) / 12, column 4 ((64 m + lane) % 12).
-        float* st = reinterpret_cast<float*>(lds + kSlots * kRingF4 + wave * kStageF4);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int hr = row0 + r;
-          float o0 = out[0][r], o1 = out[1][r], o2 = out[2][r];
-          if constexpr (kTrans) {
-            const int ht = min(hr, n_valid - 1);
-            o0 += trs[wave][ht * 3 + 0];
-            o1 += trs[wave][ht * 3 + 1];
-            o2 += trs[wave][ht * 3 + 2];
-          }
-          st[hr * kStageRow + 3 * col + 0] = o0;
-          st[hr * kStageRow + 3 * col + 1] = o1;
-          st[hr * kStageRow + 3 * col + 2] = o2;
-          if constexpr (kVposed)
-            store_out<false>(ptile + unsigned(min(hr, n_valid - 1) * vstride32 + voff),
-                             f32x3{p[0][r], p[1][r], p[2][r]});
-        }
-#pragma unroll
-        for (int m = 0; m < 3; ++m) {
-          const int i = 64 * m + lane;
-          const int hr = min(i / 12, n_valid - 1), c4 = 4 * (i % 12);  // rows past the batch: the last hand again
-          const f32x4 v = *reinterpret_cast<const f32x4*>(st + hr * kStageRow + c4);
-          float* dst = vtile + unsigned(hr * vstride32 + 3 * vb + c4);
-          if constexpr (MANO_BS_NT_STORE && !kVposed) __builtin_nontemporal_store(v, reinterpret_cast<f32x4u*>(dst));
-          else *reinterpret_cast<f32x4u*>(dst) = v;
-        }
-      } else {
       // One 12-B point store per row; rows past the batch end rewrite the
       // last hand's identical values.
 #pragma unroll
@@ -557,7 +514,6 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
         if constexpr (kVposed)
           store_out<false>(ptile + unsigned(hr * vstride32 + voff), f32x3{p[0][r], p[1][r], p[2][r]});
       }
-      }
       prio_down<kStorePrio>();
     }
   }
@@ -567,151 +523,6 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
   bs_stamp(6, (unsigned long long)n_ranges);
   bs_stamp(7, t_first | (t_prologue << 32));
 #endif
-}
-
-// ---------------------------------------------------------------------------
-// blend_skin16w: blend_skin16's arithmetic with one 12-wave block per CU
-// (3 waves per SIMD, each its own 16-hand tile, so a unit is a set of 12
-// tiles x one vertex group) sharing ONE basis ring of two group slots: the
-// block stages each group's 3 basis tiles + W fragment once for 192 hands
-// (blend_skin16: once per 64 hands, three rings per CU), every wave issues
-// exactly 3 LDS-DMA pieces per group (31 real pieces, the rest land in a
-// sink), and there is one barrier per group instead of three: group g + 1
-// is staged while group g is computed, and the barrier after g's stores
-// waits for that DMA (counted vmcnt: the stores stay in flight) and for
-// every wave to leave g's slot before g + 2 overwrites it.  Same MFMA chains
-// and apply order as blend_skin16: identical bits.
-// ---------------------------------------------------------------------------
-#ifndef MANO_BS_WIDE
-#define MANO_BS_WIDE 0
-#endif
-constexpr int kWideWaves = 12;
-constexpr int kWideGroupF4 = (3 * kGroups16 + 1) * 64;   // 3 tiles + W: 31 KB
-constexpr int kWidePieces = 3;                            // DMA ops per wave and group
-static_assert(kWideWaves * kWidePieces >= 3 * kGroups16 + 1, "pieces per group");
-
-template <bool kTrans, bool kVposed>
-__global__ __launch_bounds__(64 * kWideWaves, 3) void blend_skin16w_kernel(
-    const float* __restrict__ features, const float* __restrict__ transforms,
-    const float* __restrict__ basis16, const float* __restrict__ wfrag16,
-    const float* __restrict__ trans, float* __restrict__ verts, float* __restrict__ vposed,
-    int64_t n, int n_verts, int n_groups) {
-  constexpr int kStores = kVposed ? 8 : 4;  // global_store_dwordx3 per group
-  __shared__ f32x4 lds[2 * kWideGroupF4];
-  __shared__ f32x4 sink[64];                 // the padding pieces land here
-  __shared__ float trs[kWideWaves][16 * 3];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int vstride32 = 3 * n_verts;
-  const int64_t nt16 = (n + 15) / 16;
-  const int64_t n_sets = (nt16 + kWideWaves - 1) / kWideWaves;
-  int64_t u, u_end;
-  unit_range(n_sets * n_groups, blockIdx.x, gridDim.x, u, u_end);
-
-  // Piece p = 3 wave + i of group grp: p < 30 basis tile p / 10, K-group
-  // p % 10; p == 30 the W fragment; p > 30 the sink (a valid 1-KB read).
-  auto stage_group = [&](int grp, f32x4* slot, int lane) {
-    unsigned lane_off = unsigned(lane) * 16u;
-    asm volatile("" : "+v"(lane_off));
-    const char* bsrc = reinterpret_cast<const char*>(basis16 + int64_t(3 * grp) * kTile16Floats);
-    const char* wsrc = reinterpret_cast<const char*>(wfrag16 + int64_t(grp) * kWFrag16Floats);
-#pragma unroll
-    for (int i = 0; i < kWidePieces; ++i) {
-      const int p = kWidePieces * wave + i;
-      const char* src;
-      f32x4* dst;
-      if (p < 3 * kGroups16) {
-        src = bsrc + unsigned(p) * 1024u;   // tile p / 10, K-group p % 10: contiguous 1-KB pieces
-        dst = slot + p * 64;
-      } else if (p == 3 * kGroups16) {
-        src = wsrc;
-        dst = slot + 3 * kGroups16 * 64;
-      } else {
-        src = wsrc;
-        dst = sink;
-      }
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + lane_off),
-                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-    }
-  };
-
-  while (u < u_end) {
-    const int64_t set = u / n_groups;
-    const int g0 = int(u - set * n_groups);
-    const int g1 = int(n_groups - g0 < u_end - u ? n_groups : g0 + (u_end - u));
-    u += g1 - g0;
-    const int64_t h0 = min(set * kWideWaves + wave, nt16 - 1) * 16;
-    const int n_valid = int(n - h0 < 16 ? n - h0 : 16);
-    int lane = threadIdx.x & 63;
-    asm volatile("" : "+v"(lane));
-    const int row0 = 4 * (lane >> 4);
-    const int col = lane & 15;
-
-    float a[kGroups16 * 4];
-    float F[12][4];
-    const int64_t row = min(h0 + (lane & 15), n - 1);
-    const f32x4* src = reinterpret_cast<const f32x4*>(features + row * kXStride) + (lane >> 4);
-#pragma unroll
-    for (int g = 0; g < kGroups16; ++g) {
-      const f32x4 v = src[4 * g];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) a[4 * g + q] = v[q];
-    }
-    load_lbs_frags(transforms, h0, n, lane, F);
-    if constexpr (kTrans) {
-      if (lane < 48) {
-        const int64_t h = h0 + lane / 3;
-        trs[wave][lane] = trans[(h < n ? h : n - 1) * 3 + lane % 3];
-      }
-    }
-    float* vtile = verts + h0 * int64_t(vstride32);
-    float* ptile = kVposed ? vposed + h0 * int64_t(vstride32) : nullptr;
-
-    stage_group(g0, lds, lane);
-    barrier_vmcnt<0>();  // group g0's slot and every prologue load have landed
-
-    for (int grp = g0; grp < g1; ++grp) {
-      int glane = threadIdx.x & 63;  // opaque per group: no lane address kept live across the loop
-      asm volatile("" : "+v"(glane));
-      f32x4* slot = lds + ((grp - g0) & 1) * kWideGroupF4;
-      // read before the next group's DMA is issued (hipcc cannot tell the
-      // slots apart and would wait for the DMA before a later read)
-      const f32x4 wf = slot[3 * kGroups16 * 64 + glane];
-      prio_up<MANO_BS_DMA_PRIO>();
-      if (grp + 1 < g1) stage_group(grp + 1, lds + ((grp + 1 - g0) & 1) * kWideGroupF4, glane);
-      prio_down<MANO_BS_DMA_PRIO>();
-      __builtin_amdgcn_sched_barrier(0);
-      f32x4 p[3];
-      p[0] = mfma16_tile(a, slot, glane);
-      __builtin_amdgcn_sched_barrier(0);
-      p[1] = mfma16_tile(a, slot + kGroups16 * 64, glane);
-      __builtin_amdgcn_sched_barrier(0);
-      p[2] = mfma16_tile(a, slot + 2 * kGroups16 * 64, glane);
-      __builtin_amdgcn_sched_barrier(0);
-      int vb = grp * 16;
-      if (vb > n_verts - 16) vb = n_verts - 16;
-      const int voff = 3 * (vb + col);
-      f32x4 out[3];
-      lbs_apply16(F, wf, p, out);
-      __builtin_amdgcn_sched_barrier(0);  // store addresses computed here, not across the chains
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int hr = min(row0 + r, n_valid - 1);
-        float o0 = out[0][r], o1 = out[1][r], o2 = out[2][r];
-        if constexpr (kTrans) {
-          o0 += trs[wave][hr * 3 + 0];
-          o1 += trs[wave][hr * 3 + 1];
-          o2 += trs[wave][hr * 3 + 2];
-        }
-        store_out<MANO_BS_NT_STORE && !kVposed>(vtile + unsigned(hr * vstride32 + voff), f32x3{o0, o1, o2});
-        if constexpr (kVposed)
-          store_out<false>(ptile + unsigned(hr * vstride32 + voff), f32x3{p[0][r], p[1][r], p[2][r]});
-      }
-      // group grp + 1's pieces have landed (only the stores are younger) and
-      // no wave still reads grp's slot, which grp + 2 is staged into next
-      if (grp + 1 < g1) barrier_vmcnt<kStores>();
-    }
-    barrier_vmcnt<kStores>();  // the range's last slot is free for the next range's prologue
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -918,23 +729,6 @@ hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* featu
                        dim3(256), 0, stream, features, transforms, m.basis16, m.wfrag16, trans, verts,
                        vposed, n, m.n_verts, m.n_groups16);
   };
-#if MANO_BS_WIDE
-  const int64_t n_sets = ((n + 15) / 16 + kWideWaves - 1) / kWideWaves;
-  auto launch_w = [&](auto kernel) {
-    int b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, 64 * kWideWaves, 0) != hipSuccess || b < 1) b = 1;
-    const int64_t cap = int64_t(1) * (m.n_cu > 0 ? m.n_cu : 1);
-    const int64_t want = (n_sets * m.n_groups16 + kMinUnitsPerWorker - 1) / kMinUnitsPerWorker;
-    hipLaunchKernelGGL(kernel, dim3(unsigned(want < cap ? want : cap)), dim3(64 * kWideWaves), 0, stream,
-                       features, transforms, m.basis16, m.wfrag16, trans, verts, vposed, n, m.n_verts,
-                       m.n_groups16);
-  };
-  if (trans && vposed) launch_w(blend_skin16w_kernel<true, true>);
-  else if (trans) launch_w(blend_skin16w_kernel<true, false>);
-  else if (vposed) launch_w(blend_skin16w_kernel<false, true>);
-  else launch_w(blend_skin16w_kernel<false, false>);
-  return hipGetLastError();
-#endif
   if (trans && vposed) launch(blend_skin16_kernel<true, true>);
   else if (trans) launch(blend_skin16_kernel<true, false>);
   else if (vposed) launch(blend_skin16_kernel<false, true>);
