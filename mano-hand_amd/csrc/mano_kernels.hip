@@ -164,6 +164,30 @@ __device__ __forceinline__ f32x4 mfma16_tile(const float (&a)[kGroups16 * 4],
   return acc;
 }
 
+// mfma16_tile with hook() issued after K-group kAt (pinned between the
+// groups' MFMAs by the scheduling barriers).
+template <int kAt, typename Hook>
+__device__ __forceinline__ f32x4 mfma16_tile_hook(const float (&a)[kGroups16 * 4],
+                                                  const f32x4* __restrict__ b, int lane, Hook&& hook) {
+  f32x4 acc = {};
+  f32x4 bn = b[lane];
+#pragma unroll
+  for (int g = 0; g < kGroups16; ++g) {
+    const f32x4 bv = bn;
+    if (g + 1 < kGroups16) bn = b[(g + 1) * 64 + lane];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (4 * g + q < kSteps16) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[4 * g + q], bv[q], acc, 0, 0, 0);
+    if (g == kAt) {
+      __builtin_amdgcn_sched_barrier(0);
+      hook();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  return acc;
+}
+
 // LBS A fragments of a 16-hand tile straight from the [n][16][3][4]
 // transforms: F[c * 4 + k][q] = A_j(hand h0 + (lane & 15))[c][k], joint
 // j = 4 q + (lane >> 4) (rows past the batch end repeat the last hand).
@@ -312,6 +336,9 @@ __device__ __forceinline__ void bs_barrier() {
 #ifndef MANO_BS_NT_STORE
 #define MANO_BS_NT_STORE 1
 #endif
+__device__ __forceinline__ float* byte_at(float* base, unsigned byte_off) {
+  return reinterpret_cast<float*>(reinterpret_cast<char*>(base) + byte_off);
+}
 template <bool kNt>
 __device__ __forceinline__ void store_out(float* dst, f32x3 v) {
   if constexpr (kNt) __builtin_nontemporal_store(v, reinterpret_cast<f32x3*>(dst));
@@ -364,6 +391,13 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
   // group's first tile, the previous group's stores.
   constexpr int kPieces = kGroups16 / 4;     // LDS-DMA pieces per wave and tile, at least
   constexpr int kDmaPrio = MANO_BS_DMA_PRIO, kStorePrio = MANO_BS_STORE_PRIO;
+  // With rest_verts (two output streams) a group's rest_verts points leave
+  // right after its GEMM tiles and its verts points inside the next group's
+  // first tile chain (after K-group 2), so the 8 stores of a group do not
+  // issue as one burst (0.605 vs 0.619 ms, same box; the verts-only kernel
+  // spills under the extra live registers and keeps its stores together).
+  constexpr bool kDefer = kVposed;
+  constexpr int kDeferAt = 2;
   __shared__ f32x4 lds[kSlots * kRingF4];
   __shared__ float trs[4][16 * 3];  // the wave's 16 translations, read back at the stores
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -451,6 +485,12 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
     }
 #endif
 
+    f32x3 pend[4];      // kDefer: the previous group's verts points, stored during this group's tile 0
+    unsigned poff[4];
+    auto flush = [&]() {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) store_out<MANO_BS_NT_STORE && !kVposed>(byte_at(vtile, poff[r]), pend[r]);
+    };
     for (int grp = g0; grp < g1; ++grp) {
       const bool more = grp + 1 < g1;
       f32x4 p[3];
@@ -459,7 +499,8 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
       if constexpr (!(MANO_BS_ABLATE & 16)) stage_basis_tile16(basis16, 3 * grp + 2, lds + 2 * kRingF4, wave, lane);
       prio_down<kDmaPrio>();
       const f32x4 wf = lds[kGroups16 * 64 + lane];  // read before slot 0 is re-staged
-      p[0] = mfma16_tile(a, lds, lane);
+      if (!kDefer || grp == g0) p[0] = mfma16_tile(a, lds, lane);
+      else p[0] = mfma16_tile_hook<kDeferAt>(a, lds, lane, flush);
       if (grp == g0) bs_barrier<kPieces>();
       else bs_barrier<kPieces + kStores>();
       if (more) {
@@ -482,6 +523,14 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
       int vb = grp * 16;
       if (vb > n_verts - 16) vb = n_verts - 16;
       const int voff = 3 * (vb + col);
+      if constexpr (kVposed) {
+        // rest_verts leave before the LBS: their stores drain under its MFMAs
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int hr = min(row0 + r, n_valid - 1);
+          store_out<false>(byte_at(ptile, 4u * unsigned(hr * vstride32 + voff)), f32x3{p[0][r], p[1][r], p[2][r]});
+        }
+      }
       f32x4 out[3];
       if constexpr (MANO_BS_ABLATE & 2) {
         out[0] = p[0];
@@ -507,15 +556,23 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
           o1 += trs[wave][hr * 3 + 1];
           o2 += trs[wave][hr * 3 + 2];
         }
+        // 32-bit byte offset from the tile's uniform base (< 16 rows x 9,336 B):
+        // the SGPR-base + VGPR-offset store form, no 64-bit address VALU.
+        // (opaque: hipcc otherwise hoists the row offsets and spills 10 VGPRs
+        // in the verts-only range prologue)
+        unsigned boff = 4u * unsigned(hr * vstride32 + voff);
+        asm volatile("" : "+v"(boff));
         if constexpr (MANO_BS_ABLATE == 4)  // needs a verts buffer of n * 49 * 256 B
           *reinterpret_cast<f32x3*>(verts + ((h0 + hr) * n_groups + grp) * 64 + 3 * col) = f32x3{o0, o1, o2};
-        else
-          store_out<MANO_BS_NT_STORE && !kVposed>(vtile + unsigned(hr * vstride32 + voff), f32x3{o0, o1, o2});
-        if constexpr (kVposed)
-          store_out<false>(ptile + unsigned(hr * vstride32 + voff), f32x3{p[0][r], p[1][r], p[2][r]});
+        else if constexpr (kDefer) {
+          pend[r] = f32x3{o0, o1, o2};
+          poff[r] = boff;
+        } else
+          store_out<MANO_BS_NT_STORE && !kVposed>(byte_at(vtile, boff), f32x3{o0, o1, o2});
       }
       prio_down<kStorePrio>();
     }
+    if constexpr (kDefer) flush();  // the range's last group
   }
 #if MANO_BS_STAMP
   bs_stamp(1, __builtin_amdgcn_s_memtime());

@@ -19,7 +19,7 @@ pose = 0.5 * torch.randn((B, 16, 3), generator=g, device=dev)
 m = ManoHip(synthetic_params(0), device=0)
 v = torch.empty((B, 778, 3), device=dev)
 m.stage_articulate(betas, pose)
-for _ in range(300):
+for _ in range(int(os.environ.get("WARM", 300))):
     m.stage_blend_skin(B, v)
 torch.cuda.synchronize()
 lib = ctypes.CDLL(_abi.LIB_PATH)
