@@ -397,6 +397,11 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
   // issue as one burst (0.605 vs 0.619 ms, same box; the verts-only kernel
   // spills under the extra live registers and keeps its stores together).
   constexpr bool kDefer = kVposed;
+  // nontemporal only with one output stream (beside the rest_verts stream
+  // either one nontemporal took 0.71 vs 0.61 ms, both 0.86:
+  // profiles/r03m_ab_rest_nt.jsonl)
+  constexpr bool kVertsNt = MANO_BS_NT_STORE && !kVposed;
+  constexpr bool kRestNt = false;
   constexpr int kDeferAt = 2;
   __shared__ f32x4 lds[kSlots * kRingF4];
   __shared__ float trs[4][16 * 3];  // the wave's 16 translations, read back at the stores
@@ -489,7 +494,7 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
     unsigned poff[4];
     auto flush = [&]() {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) store_out<MANO_BS_NT_STORE && !kVposed>(byte_at(vtile, poff[r]), pend[r]);
+      for (int r = 0; r < 4; ++r) store_out<kVertsNt>(byte_at(vtile, poff[r]), pend[r]);
     };
     for (int grp = g0; grp < g1; ++grp) {
       const bool more = grp + 1 < g1;
@@ -528,7 +533,7 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int hr = min(row0 + r, n_valid - 1);
-          store_out<false>(byte_at(ptile, 4u * unsigned(hr * vstride32 + voff)), f32x3{p[0][r], p[1][r], p[2][r]});
+          store_out<kRestNt>(byte_at(ptile, 4u * unsigned(hr * vstride32 + voff)), f32x3{p[0][r], p[1][r], p[2][r]});
         }
       }
       f32x4 out[3];
@@ -568,7 +573,7 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
           pend[r] = f32x3{o0, o1, o2};
           poff[r] = boff;
         } else
-          store_out<MANO_BS_NT_STORE && !kVposed>(byte_at(vtile, boff), f32x3{o0, o1, o2});
+          store_out<kVertsNt>(byte_at(vtile, boff), f32x3{o0, o1, o2});
       }
       prio_down<kStorePrio>();
     }
