@@ -4,13 +4,17 @@
 
 path: unfused (articulate, blend, skin), skin_b2b (the LBS alone, back to
 back), staged (articulate, blend_skin16), rest_verts (blend_skin16 with
-rest_verts).  65,536 hands of C2 inputs by default."""
+rest_verts).  65,536 hands of C2 inputs by default; MANO_LIB=<name> loads
+mano_amd/<name> instead of libmano_hip.so."""
 import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(REPO, "mano-hand_amd"), REPO]
 import torch  # noqa: E402
+from mano_amd import _abi  # noqa: E402
+if os.environ.get("MANO_LIB"):  # another build of the library (A/B), in mano_amd/
+    _abi.LIB_PATH = os.path.join(os.path.dirname(_abi.LIB_PATH), os.environ["MANO_LIB"])
 from mano_amd import ManoHip, synthetic_params  # noqa: E402
 
 path = sys.argv[1]
