@@ -80,11 +80,14 @@ constexpr int kQTrF4 = kQHands * kQTrF4PerHand / 64;         // 3 float4 per lan
 constexpr int kQMaxGroups = MANO_QUAD_MAX_GROUPS;
 static_assert(kQHands * kQRowF4 % 64 == 0 && kQHands * kQTrF4PerHand % 64 == 0, "whole sweeps");
 
-struct QuadStage {
-  float rows[kQHands * kQStride];         // the unit's v_posed rows, then its verts
+template <int kStride>
+struct StageT {
+  static constexpr int kRowStride = kStride;
+  float rows[kQHands * kStride];          // the unit's v_posed rows, then its verts
   float tr[kQHands * kTransformFloats];   // the 4 hands' [16][3][4] transforms
   float trans[16];                        // the 4 hands' translations (12 used)
 };
+using QuadStage = StageT<kQStride>;
 
 // c ? a : b on values (a select of array elements can become a select of
 // their addresses, which sends the arrays to scratch).
@@ -100,8 +103,8 @@ __device__ __forceinline__ void wave_sync() {
 
 // NG groups (G[0..NG)): the full units and a 1-group tail skip the
 // duplicates a multi-group tail needs.
-template <bool kTrans, int NG = 4>
-__device__ __forceinline__ void skin_unit4_w(QuadStage& st, const f32x4 (&wf)[4], const float (&a)[3][4],
+template <bool kTrans, int NG = 4, class Stage = QuadStage>
+__device__ __forceinline__ void skin_unit4_w(Stage& st, const f32x4 (&wf)[4], const float (&a)[3][4],
                                              const float (&tr3)[3], const int (&lv)[4], const int (&hh)[3],
                                              const int (&cc)[3], int v) {
   float p[NG][3][3];
@@ -110,7 +113,7 @@ __device__ __forceinline__ void skin_unit4_w(QuadStage& st, const f32x4 (&wf)[4]
 #pragma unroll
     for (int t = 0; t < 3; ++t)
 #pragma unroll
-      for (int c = 0; c < 3; ++c) p[g][t][c] = st.rows[hh[t] * kQStride + 3 * (lv[g] + v) + c];
+      for (int c = 0; c < 3; ++c) p[g][t][c] = st.rows[hh[t] * Stage::kRowStride + 3 * (lv[g] + v) + c];
 #if MANO_QUAD_P_EARLY
   // The point reads issue before the MFMAs and land behind them (hipcc would
   // sink them below the MFMAs to save registers, exposing their latency).
@@ -135,7 +138,7 @@ __device__ __forceinline__ void skin_unit4_w(QuadStage& st, const f32x4 (&wf)[4]
       o = fmaf(T[t][1], p[g][t][1], o);
       o = fmaf(T[t][0], p[g][t][0], o);
       if constexpr (kTrans) o = o + tr3[t];
-      st.rows[hh[t] * kQStride + 3 * (lv[g] + v) + cc[t]] = o;
+      st.rows[hh[t] * Stage::kRowStride + 3 * (lv[g] + v) + cc[t]] = o;
     }
   }
 #else
@@ -156,20 +159,20 @@ __device__ __forceinline__ void skin_unit4_w(QuadStage& st, const f32x4 (&wf)[4]
       o = fmaf(T[g][t][1], p[g][t][1], o);
       o = fmaf(T[g][t][0], p[g][t][0], o);
       if constexpr (kTrans) o = o + tr3[t];
-      st.rows[hh[t] * kQStride + 3 * (lv[g] + v) + cc[t]] = o;
+      st.rows[hh[t] * Stage::kRowStride + 3 * (lv[g] + v) + cc[t]] = o;
     }
 #endif
 }
 
 // skin_unit4_w with the groups' W fragments read from the block's LDS copy.
-template <bool kTrans, int NG = 4>
-__device__ __forceinline__ void skin_unit4(QuadStage& st, const f32x4* w_lds, const float (&a)[3][4],
+template <bool kTrans, int NG = 4, class Stage = QuadStage>
+__device__ __forceinline__ void skin_unit4(Stage& st, const f32x4* w_lds, const float (&a)[3][4],
                                            const float (&tr3)[3], const int (&G)[4], const int (&lv)[4],
                                            const int (&hh)[3], const int (&cc)[3], int v, int lane) {
   f32x4 wf[4];
 #pragma unroll
   for (int g = 0; g < NG; ++g) wf[g] = w_lds[G[g] * 64 + lane];
-  skin_unit4_w<kTrans, NG>(st, wf, a, tr3, lv, hh, cc, v);
+  skin_unit4_w<kTrans, NG, Stage>(st, wf, a, tr3, lv, hh, cc, v);
 }
 
 // The f16x3 precision mode (mano_kernels_h3.hip) on the same units: the
@@ -182,8 +185,8 @@ __device__ __forceinline__ void skin_unit4(QuadStage& st, const f32x4* w_lds, co
 // wl: per group 64 x 16 B, entries 0-31 = w1's lanes 0-31 (lanes 32-63 are
 // the same), 32-63 = w2's lanes 0-31 (lanes 32-63 are zero).
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-template <bool kTrans, int NG = 4>
-__device__ __forceinline__ void skin_unit4_h3(QuadStage& st, const f16x8* wl, const f16x8 (&a)[3],
+template <bool kTrans, int NG = 4, class Stage = QuadStage>
+__device__ __forceinline__ void skin_unit4_h3(Stage& st, const f16x8* wl, const f16x8 (&a)[3],
                                               const float (&tr3)[3], const int (&G)[4], const int (&lv)[4],
                                               const int (&hh)[3], const int (&cc)[3], int v, int lane,
                                               float t_unscale) {
@@ -193,7 +196,7 @@ __device__ __forceinline__ void skin_unit4_h3(QuadStage& st, const f16x8* wl, co
 #pragma unroll
     for (int t = 0; t < 3; ++t)
 #pragma unroll
-      for (int c = 0; c < 3; ++c) p[g][t][c] = st.rows[hh[t] * kQStride + 3 * (lv[g] + v) + c];
+      for (int c = 0; c < 3; ++c) p[g][t][c] = st.rows[hh[t] * Stage::kRowStride + 3 * (lv[g] + v) + c];
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
@@ -211,7 +214,7 @@ __device__ __forceinline__ void skin_unit4_h3(QuadStage& st, const f16x8* wl, co
       o = fmaf(T[t][2], p[g][t][2], o);
       o = fmaf(T[t][1], p[g][t][1], o);
       o = fmaf(T[t][0], p[g][t][0], o);
-      st.rows[hh[t] * kQStride + 3 * (lv[g] + v) + cc[t]] = fmaf(o, t_unscale, kTrans ? tr3[t] : 0.f);
+      st.rows[hh[t] * Stage::kRowStride + 3 * (lv[g] + v) + cc[t]] = fmaf(o, t_unscale, kTrans ? tr3[t] : 0.f);
     }
   }
 }
@@ -451,9 +454,16 @@ constexpr int kPairWaves = kPairs * (1 + kPairCompute);
 #endif
 constexpr bool kPairReverse = MANO_PAIR_REVERSE;
 constexpr int kPairMaxGroups = 52;  // W in LDS beside the slots: V <= 832
+#ifndef MANO_PAIR_PACKED
+#define MANO_PAIR_PACKED 0  // unit rows packed at 192 floats: 3 full-wave row DMAs per unit instead of 4
+#endif
+constexpr bool kPairPacked = MANO_PAIR_PACKED;
+using PairStage = StageT<kPairPacked ? 3 * kQVerts : kQStride>;
+constexpr int kPStride = PairStage::kRowStride;
+constexpr int kPairRowDmas = kPairPacked ? kQHands * kQRowF4 / 64 : kQHands;
 
 struct PairShared {
-  QuadStage slot[kPairs][kPairSlots];
+  PairStage slot[kPairs][kPairSlots];
   int full[kPairs];               // units staged
   int done[kPairs][kPairSlots];   // per slot: 1 + the last unit skinned in it
 };
@@ -601,6 +611,9 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     }
   };
   const int tail_v0 = min(kQVerts * n_full, n_verts - 16);
+  // packed rows: a tail unit stages the 64-vertex window ending at the mesh
+  // end (its first vertices are the previous span's: read, never stored)
+  const int tw0 = kPairPacked ? max(0, n_verts - kQVerts) : tail_v0;
   int* full_flag = &sh.full[pair];
   int64_t qd = worker / spans;
   int s = int(worker - qd * spans);
@@ -620,6 +633,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     // Rows and hands past the batch end fall outside num_records: their
     // loads write zeros, their stores are dropped.
     const int tail_rf4 = 3 * (n_verts - tail_v0) / 4;
+    const int toff = 3 * (tail_v0 - tw0);     // the tail vertices' float offset in a staged row
     int fvo[kQF4], tvo[kQF4];                 // store sweep: global byte offsets in the unit's rows
     unsigned fso[kQF4], tso[kQF4];            // store sweep: LDS byte addresses in slot 0
     const unsigned slot0 = lds_addr(reinterpret_cast<const int*>(&sh.slot[pair][0]));
@@ -631,51 +645,65 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       const int tr = it / tail_rf4, tc = 4 * (it % tail_rf4);
       fvo[i] = 4 * (fr * vstride + fc);
       tvo[i] = 4 * (tr * vstride + tc);
-      fso[i] = slot0 + unsigned(offsetof(QuadStage, rows)) + 4u * unsigned(fr * kQStride + fc);
-      tso[i] = slot0 + unsigned(offsetof(QuadStage, rows)) + 4u * unsigned(tr * kQStride + tc);
+      fso[i] = slot0 + unsigned(offsetof(PairStage, rows)) + 4u * unsigned(fr * kPStride + fc);
+      tso[i] = slot0 + unsigned(offsetof(PairStage, rows)) + 4u * unsigned(tr * kPStride + toff + tc);
     }
-    int rvo[kQHands];  // DMA: lane's byte offset in row r of the unit
+    int rvo[kPairRowDmas];  // DMA j: the lane's byte offset in the unit's rows
 #pragma unroll
-    for (int r = 0; r < kQHands; ++r) rvo[r] = 4 * r * vstride + 16 * lane;
+    for (int j = 0; j < kPairRowDmas; ++j) {
+      if constexpr (kPairPacked) {
+        const int idx = 64 * j + lane;  // LDS float4 slot idx = (row idx / 48, float4 idx % 48)
+        rvo[j] = 4 * (idx / kQRowF4) * vstride + 16 * (idx % kQRowF4);
+      } else {
+        rvo[j] = 4 * j * vstride + 16 * lane;
+      }
+    }
     constexpr int kRsrcFlags = 0x00020000;  // gfx9 raw buffer
     auto rsrc = [&](const float* base, int64_t floats) {
       return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, int(floats * 4), kRsrcFlags);
     };
     const unsigned slot0_s = __builtin_amdgcn_readfirstlane(slot0);
     auto lds_at = [&](int slot, unsigned byte_off) {
-      return slot0_s + unsigned(slot) * unsigned(sizeof(QuadStage)) + byte_off;
+      return slot0_s + unsigned(slot) * unsigned(sizeof(PairStage)) + byte_off;
     };
     // VMEM ops per DMA: 4 rows + 3 transform sweeps (+ 1 translations)
     // (diagnostic MANO_QUAD_ABLATE & 4: no transform DMA -- stale operands, timing only)
     constexpr int kTrOps = (MANO_QUAD_ABLATE & 4) ? 0 : kQTrF4;
-    constexpr int kDmaOps = kQHands + kTrOps + (kTrans ? 1 : 0);
+    constexpr int kDmaOps = kPairRowDmas + kTrOps + (kTrans ? 1 : 0);
     auto dma = [&](int64_t fq, int fs, int slot) {
       const int64_t h0 = (kPairReverse ? n_quads - 1 - fq : fq) * kQHands;
       const int valid = int(n - h0 < kQHands ? n - h0 : kQHands);
       const auto rv = rsrc(vposed + h0 * vstride, int64_t(valid) * vstride);
       const auto rt = rsrc(transforms + h0 * kTransformFloats, int64_t(valid) * kTransformFloats);
       const bool full = fs < n_full;
-      const int soff = 4 * 3 * (full ? kQVerts * fs : tail_v0);
+      const int soff = 4 * 3 * (full ? kQVerts * fs : tw0);
       const int row_f4 = full ? kQRowF4 : tail_rf4;
 #pragma unroll
       for (int i = 0; i < kTrOps; ++i)
-        buffer_load_lds16(rt, lds_at(slot, unsigned(offsetof(QuadStage, tr)) + 1024u * i), 16 * lane,
+        buffer_load_lds16(rt, lds_at(slot, unsigned(offsetof(PairStage, tr)) + 1024u * i), 16 * lane,
                                        1024 * i);
       if constexpr (kTrans) {
         const auto rr = rsrc(trans + h0 * 3, int64_t(valid) * 3);
         if (lane < 12)
-          buffer_load_lds4(rr, lds_at(slot, unsigned(offsetof(QuadStage, trans))), 4 * lane, 0);
+          buffer_load_lds4(rr, lds_at(slot, unsigned(offsetof(PairStage, trans))), 4 * lane, 0);
       }
+      if constexpr (kPairPacked) {
+        (void)row_f4;
 #pragma unroll
-      for (int r = 0; r < kQHands; ++r)
-        if (lane < row_f4)
-          buffer_load_lds16(rv, lds_at(slot, unsigned(offsetof(QuadStage, rows)) + 4u * r * kQStride),
-                                           rvo[r], soff);
+        for (int j = 0; j < kPairRowDmas; ++j)
+          buffer_load_lds16(rv, lds_at(slot, unsigned(offsetof(PairStage, rows)) + 1024u * j), rvo[j], soff);
+      } else {
+#pragma unroll
+        for (int r = 0; r < kQHands; ++r)
+          if (lane < row_f4)
+            buffer_load_lds16(rv, lds_at(slot, unsigned(offsetof(PairStage, rows)) + 4u * r * kPStride),
+                                             rvo[r], soff);
+      }
     };
     auto ds_read4 = [](unsigned addr) {
       return *reinterpret_cast<const __attribute__((address_space(3))) f32x4*>(uintptr_t(addr));
     };
-    constexpr unsigned kSlotBytes = sizeof(QuadStage);
+    constexpr unsigned kSlotBytes = sizeof(PairStage);
     auto store = [&](int64_t fq, int fs, unsigned slot, bool real) {
       const unsigned so = slot * kSlotBytes;
       const int64_t h0 = (kPairReverse ? n_quads - 1 - fq : fq) * kQHands;
@@ -711,6 +739,10 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
 #pragma unroll
     for (int j = 1; j < kAhead; ++j) {
       store(qd, s, 0, false);
+      // the dropped stores stay ahead of the next DMA group (nothing else
+      // orders them: no data dependence, no exec-masked block in between)
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
       dma(qa < n_quads ? qa : qd, qa < n_quads ? sa : s, j);
       advance(qa, sa);
     }
@@ -740,6 +772,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       // the store's LDS reads have returned (its data is in registers), so
       // unit k - 2's slot is free for unit k + kAhead
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
       PAIR_TIMED_STMT(dma(qa < n_quads ? qa : qd, qa < n_quads ? sa : s, (k + kAhead) % kPairSlots), t_fetch);
       advance(qa, sa);
       advance(qd, s);
@@ -780,7 +813,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       return;
     }
     ++stamp.units;
-    QuadStage& st = sh.slot[pair][k % kPairSlots];
+    PairStage& st = sh.slot[pair][k % kPairSlots];
     if (MANO_QUAD_ABLATE & 2) {  // diagnostic: no compute (the memory waves alone)
       pair_signal(&sh.done[pair][k % kPairSlots], k + 1);
 #pragma unroll
@@ -815,16 +848,16 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       if (s < n_full) {
         const int G[4] = {4 * s, 4 * s + 1, 4 * s + 2, 4 * s + 3};
         const int lv[4] = {0, 16, 32, 48};
-        skin_unit4_h3<kTrans>(st, wl, ah, tr3, G, lv, hh, cc, v, lane, t_unscale);
+        skin_unit4_h3<kTrans, 4, PairStage>(st, wl, ah, tr3, G, lv, hh, cc, v, lane, t_unscale);
       } else {
         int G[4], lv[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           G[g] = 4 * n_full + min(g, n_tail - 1);
-          lv[g] = min(16 * G[g], n_verts - 16) - tail_v0;
+          lv[g] = min(16 * G[g], n_verts - 16) - tw0;
         }
-        if (n_tail == 1) skin_unit4_h3<kTrans, 1>(st, wl, ah, tr3, G, lv, hh, cc, v, lane, t_unscale);
-        else skin_unit4_h3<kTrans>(st, wl, ah, tr3, G, lv, hh, cc, v, lane, t_unscale);
+        if (n_tail == 1) skin_unit4_h3<kTrans, 1, PairStage>(st, wl, ah, tr3, G, lv, hh, cc, v, lane, t_unscale);
+        else skin_unit4_h3<kTrans, 4, PairStage>(st, wl, ah, tr3, G, lv, hh, cc, v, lane, t_unscale);
       }
     } else {
       float a[3][4];
@@ -835,16 +868,16 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       if (s < n_full) {
         const int G[4] = {4 * s, 4 * s + 1, 4 * s + 2, 4 * s + 3};
         const int lv[4] = {0, 16, 32, 48};
-        skin_unit4<kTrans>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
+        skin_unit4<kTrans, 4, PairStage>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
       } else {
         int G[4], lv[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           G[g] = 4 * n_full + min(g, n_tail - 1);
-          lv[g] = min(16 * G[g], n_verts - 16) - tail_v0;
+          lv[g] = min(16 * G[g], n_verts - 16) - tw0;
         }
-        if (n_tail == 1) skin_unit4<kTrans, 1>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
-        else skin_unit4<kTrans>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
+        if (n_tail == 1) skin_unit4<kTrans, 1, PairStage>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
+        else skin_unit4<kTrans, 4, PairStage>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
       }
     }
     pair_signal(&sh.done[pair][k % kPairSlots], k + 1);
