@@ -454,13 +454,12 @@ constexpr int kPairWaves = kPairs * (1 + kPairCompute);
 #endif
 constexpr bool kPairReverse = MANO_PAIR_REVERSE;
 constexpr int kPairMaxGroups = 52;  // W in LDS beside the slots: V <= 832
-#ifndef MANO_PAIR_PACKED
-#define MANO_PAIR_PACKED 0  // unit rows packed at 192 floats: 3 full-wave row DMAs per unit instead of 4
-#endif
-constexpr bool kPairPacked = MANO_PAIR_PACKED;
-using PairStage = StageT<kPairPacked ? 3 * kQVerts : kQStride>;
+// (Rows packed at 192 floats, DMA'd as 3 full-wave instructions per unit
+// instead of 4 three-quarter-wave ones: measured no faster, commit 05d3853,
+// profiles/r03n_ab_skin_packed.jsonl.)
+using PairStage = QuadStage;
 constexpr int kPStride = PairStage::kRowStride;
-constexpr int kPairRowDmas = kPairPacked ? kQHands * kQRowF4 / 64 : kQHands;
+constexpr int kPairRowDmas = kQHands;
 
 struct PairShared {
   PairStage slot[kPairs][kPairSlots];
@@ -611,9 +610,6 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     }
   };
   const int tail_v0 = min(kQVerts * n_full, n_verts - 16);
-  // packed rows: a tail unit stages the 64-vertex window ending at the mesh
-  // end (its first vertices are the previous span's: read, never stored)
-  const int tw0 = kPairPacked ? max(0, n_verts - kQVerts) : tail_v0;
   int* full_flag = &sh.full[pair];
   int64_t qd = worker / spans;
   int s = int(worker - qd * spans);
@@ -633,7 +629,6 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     // Rows and hands past the batch end fall outside num_records: their
     // loads write zeros, their stores are dropped.
     const int tail_rf4 = 3 * (n_verts - tail_v0) / 4;
-    const int toff = 3 * (tail_v0 - tw0);     // the tail vertices' float offset in a staged row
     int fvo[kQF4], tvo[kQF4];                 // store sweep: global byte offsets in the unit's rows
     unsigned fso[kQF4], tso[kQF4];            // store sweep: LDS byte addresses in slot 0
     const unsigned slot0 = lds_addr(reinterpret_cast<const int*>(&sh.slot[pair][0]));
@@ -646,18 +641,11 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       fvo[i] = 4 * (fr * vstride + fc);
       tvo[i] = 4 * (tr * vstride + tc);
       fso[i] = slot0 + unsigned(offsetof(PairStage, rows)) + 4u * unsigned(fr * kPStride + fc);
-      tso[i] = slot0 + unsigned(offsetof(PairStage, rows)) + 4u * unsigned(tr * kPStride + toff + tc);
+      tso[i] = slot0 + unsigned(offsetof(PairStage, rows)) + 4u * unsigned(tr * kPStride + tc);
     }
     int rvo[kPairRowDmas];  // DMA j: the lane's byte offset in the unit's rows
 #pragma unroll
-    for (int j = 0; j < kPairRowDmas; ++j) {
-      if constexpr (kPairPacked) {
-        const int idx = 64 * j + lane;  // LDS float4 slot idx = (row idx / 48, float4 idx % 48)
-        rvo[j] = 4 * (idx / kQRowF4) * vstride + 16 * (idx % kQRowF4);
-      } else {
-        rvo[j] = 4 * j * vstride + 16 * lane;
-      }
-    }
+    for (int j = 0; j < kPairRowDmas; ++j) rvo[j] = 4 * j * vstride + 16 * lane;
     constexpr int kRsrcFlags = 0x00020000;  // gfx9 raw buffer
     auto rsrc = [&](const float* base, int64_t floats) {
       return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, int(floats * 4), kRsrcFlags);
@@ -676,7 +664,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       const auto rv = rsrc(vposed + h0 * vstride, int64_t(valid) * vstride);
       const auto rt = rsrc(transforms + h0 * kTransformFloats, int64_t(valid) * kTransformFloats);
       const bool full = fs < n_full;
-      const int soff = 4 * 3 * (full ? kQVerts * fs : tw0);
+      const int soff = 4 * 3 * (full ? kQVerts * fs : tail_v0);
       const int row_f4 = full ? kQRowF4 : tail_rf4;
 #pragma unroll
       for (int i = 0; i < kTrOps; ++i)
@@ -687,18 +675,11 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
         if (lane < 12)
           buffer_load_lds4(rr, lds_at(slot, unsigned(offsetof(PairStage, trans))), 4 * lane, 0);
       }
-      if constexpr (kPairPacked) {
-        (void)row_f4;
 #pragma unroll
-        for (int j = 0; j < kPairRowDmas; ++j)
-          buffer_load_lds16(rv, lds_at(slot, unsigned(offsetof(PairStage, rows)) + 1024u * j), rvo[j], soff);
-      } else {
-#pragma unroll
-        for (int r = 0; r < kQHands; ++r)
-          if (lane < row_f4)
-            buffer_load_lds16(rv, lds_at(slot, unsigned(offsetof(PairStage, rows)) + 4u * r * kPStride),
-                                             rvo[r], soff);
-      }
+      for (int r = 0; r < kQHands; ++r)
+        if (lane < row_f4)
+          buffer_load_lds16(rv, lds_at(slot, unsigned(offsetof(PairStage, rows)) + 4u * r * kPStride),
+                                           rvo[r], soff);
     };
     auto ds_read4 = [](unsigned addr) {
       return *reinterpret_cast<const __attribute__((address_space(3))) f32x4*>(uintptr_t(addr));
@@ -854,7 +835,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           G[g] = 4 * n_full + min(g, n_tail - 1);
-          lv[g] = min(16 * G[g], n_verts - 16) - tw0;
+          lv[g] = min(16 * G[g], n_verts - 16) - tail_v0;
         }
         if (n_tail == 1) skin_unit4_h3<kTrans, 1, PairStage>(st, wl, ah, tr3, G, lv, hh, cc, v, lane, t_unscale);
         else skin_unit4_h3<kTrans, 4, PairStage>(st, wl, ah, tr3, G, lv, hh, cc, v, lane, t_unscale);
@@ -874,7 +855,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           G[g] = 4 * n_full + min(g, n_tail - 1);
-          lv[g] = min(16 * G[g], n_verts - 16) - tw0;
+          lv[g] = min(16 * G[g], n_verts - 16) - tail_v0;
         }
         if (n_tail == 1) skin_unit4<kTrans, 1, PairStage>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
         else skin_unit4<kTrans, 4, PairStage>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
