@@ -148,24 +148,10 @@ __global__ __launch_bounds__(256, 2) void blend_kernel(
 // each other's barrier / LDS / store stalls.
 // ---------------------------------------------------------------------------
 typedef float f32x4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ f32x4 mfma16_tile(const float (&a)[kGroups16 * 4],
-                                             const f32x4* __restrict__ b, int lane) {
-  f32x4 acc = {};
-  f32x4 bn = b[lane];
-#pragma unroll
-  for (int g = 0; g < kGroups16; ++g) {
-    const f32x4 bv = bn;
-    if (g + 1 < kGroups16) bn = b[(g + 1) * 64 + lane];
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (4 * g + q < kSteps16) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[4 * g + q], bv[q], acc, 0, 0, 0);
-  }
-  return acc;
-}
-
-// mfma16_tile with hook() issued after K-group kAt (pinned between the
-// groups' MFMAs by the scheduling barriers).
+// One GEMM tile: 37 dependent v_mfma_f32_16x16x4_f32 (one accumulator), the
+// LDS read of K-group g + 1 issued before group g's four MFMAs and pinned
+// there by a scheduling barrier.  hook() is issued after K-group kAt (pinned
+// between the groups' MFMAs the same way; kAt < 0: none).
 template <int kAt, typename Hook>
 __device__ __forceinline__ f32x4 mfma16_tile_hook(const float (&a)[kGroups16 * 4],
                                                   const f32x4* __restrict__ b, int lane, Hook&& hook) {
@@ -186,6 +172,10 @@ __device__ __forceinline__ f32x4 mfma16_tile_hook(const float (&a)[kGroups16 * 4
     }
   }
   return acc;
+}
+__device__ __forceinline__ f32x4 mfma16_tile(const float (&a)[kGroups16 * 4], const f32x4* __restrict__ b,
+                                             int lane) {
+  return mfma16_tile_hook<-1>(a, b, lane, [] {});
 }
 
 // LBS A fragments of a 16-hand tile straight from the [n][16][3][4]
