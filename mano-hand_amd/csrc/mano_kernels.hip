@@ -63,21 +63,24 @@ __device__ __forceinline__ f32x16 mfma_tile(const float (&a)[kKGroups * 4], cons
   return acc;
 }
 
-#ifndef MANO_BLEND_NT_STORE
-#define MANO_BLEND_NT_STORE 0  // nontemporal v_posed stores in the unfused blend GEMM
-#endif
+// v_posed leaves as buffer stores with the sc0 cache policy: the unfused blend
+// 0.3629-0.3669 vs 0.3676-0.3765 ms with plain global stores, the LBS after it
+// 0.288 vs 0.290 (same box, same bits); sc1 took the blend to 0.395
+// (profiles/r03q_ab_blend_store_policy.jsonl); nontemporal stores to 0.60
+// (partial lines: rows are 9,336 B apart).  Rows past the batch end fall
+// outside the tile's buffer and are dropped.
 __device__ __forceinline__ void store_vposed_tile(float* __restrict__ vposed, const f32x16& acc,
                                                   int64_t h0, int col, int64_t n, int n_cols,
                                                   int hi) {
   // D[hand][col]: col = lane & 31, hand = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
+  const int64_t valid = n - h0 < 32 ? n - h0 : 32;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(vposed + h0 * n_cols, 0, int(valid * n_cols * 4), 0x00020000);
   if (col < n_cols) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int64_t h = h0 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-      if (h < n) {
-        if constexpr (MANO_BLEND_NT_STORE) __builtin_nontemporal_store(acc[r], vposed + h * n_cols + col);
-        else vposed[h * n_cols + col] = acc[r];
-      }
+      const int hr = (r & 3) + 8 * (r >> 2) + 4 * hi;
+      const float x = acc[r];  // a scalar first: __builtin_bit_cast of a vector element reads element 0
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), rs, 4 * (hr * n_cols + col), 0, 1 /* sc0 */);
     }
   }
 }
