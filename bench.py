@@ -113,6 +113,16 @@ def parse(argv=None):
                     help="process-group backend for N > 1 (gloo: rehearsal, ranks may share a GPU)")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the N ranks, meet in a barrier, print the world and exit (no GPU)")
+    ap.add_argument("--force-pg", action="store_true",
+                    help="take the process-group path even at one rank (init_process_group with "
+                         "device_id, AbiGather's id broadcast, the gather, the on-device all_reduce, "
+                         "all_gather_object): a 1-GPU rehearsal of the N > 1 code, under torchrun")
+    ap.add_argument("--gather-impl", choices=("sendrecv", "allgather"), default="sendrecv",
+                    help="the timed gather: sendrecv = mano_gather (grouped RCCL send/recv, every peer "
+                         "straight to GPU 0); allgather = mano_allgather (RCCL ring all-gather)")
+    ap.add_argument("--gather-compare-reps", type=int, default=4,
+                    help="after timing, run the other gather form this many times and report it "
+                         "beside the timed one (0 = skip; RCCL only)")
     return ap.parse_args(argv)
 
 
@@ -131,13 +141,55 @@ def launch_command(argv, n):
             os.path.abspath(__file__), *argv]
 
 
-def cpu_share():
-    """CPUs this process may use, at most 16 (the GPU box's share per GPU)."""
+def cpu_share(n_gpus=1):
+    """CPUs this process may use, at most 16 per GPU of the run (the GPU box's
+    share per GPU)."""
     try:
         n = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
         n = os.cpu_count() or 1
-    return max(1, min(n, 16))
+    return max(1, min(n, 16 * max(1, n_gpus)))
+
+
+def child_device_env(env, local_dev):
+    """`env` for a child process that must see only this rank's GPU: the
+    visible-devices variable narrowed to entry `local_dev` (or set to it)."""
+    env = dict(env)
+    for var in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        if env.get(var):
+            ids = [x for x in env[var].split(",") if x.strip()]
+            if local_dev < len(ids):
+                env[var] = ids[local_dev].strip()
+            return env
+    env["HIP_VISIBLE_DEVICES"] = str(local_dev)
+    return env
+
+
+XGMI_LINK_GBS = 153.0   # one xGMI link, GB/s per direction (SURVEY.md §5; 7 links per MI355X)
+HAND_OUT_BYTES = (V * 3 + 16 * 3) * 4   # verts + posed joints of one hand = 9,528 B
+
+
+def gather_stats(impl, world, B, ms):
+    """Bandwidth figures of one gather of every rank's verts + joints (B hands
+    per rank) that took `ms` on GPU 0.  sendrecv: world - 1 peers each send
+    their shard over their own link into GPU 0 (per-link bytes = one shard);
+    allgather: RCCL's ring, every link carries world - 1 shards."""
+    shard = B * HAND_OUT_BYTES
+    to_gpu0 = (world - 1) * shard
+    if impl == "allgather":
+        links, link_bytes = world, (world - 1) * shard
+    else:
+        links, link_bytes = world - 1, shard
+    out = {"impl": impl, "ms": ms, "shard_bytes": shard, "bytes_to_gpu0": to_gpu0,
+           "bytes_landed_total": (world - 1) * shard * (world if impl == "allgather" else 1),
+           "links": links, "link_GBs_spec": XGMI_LINK_GBS}
+    if ms and ms > 0 and world > 1:
+        out["GBs_to_gpu0"] = to_gpu0 / (ms * 1e-3) / 1e9
+        out["link_GBs"] = link_bytes / (ms * 1e-3) / 1e9
+        out["link_frac"] = out["link_GBs"] / XGMI_LINK_GBS
+    else:
+        out["GBs_to_gpu0"] = out["link_GBs"] = out["link_frac"] = None
+    return out
 
 
 def cpu_baseline(procs, seconds):
@@ -324,7 +376,7 @@ def pmc_child_args(args, batch):
             "--no-cpu", "--no-extra", "--no-live-pmc", "--no-check", "--no-dropin"]
 
 
-def live_traffic(args, batch, name_fragment, timeout=120):
+def live_traffic(args, batch, name_fragment, timeout=120, local_dev=0):
     """HBM bytes per launch of the dominant kernel measured in this run: rocprofv3
     --pmc FETCH_SIZE and --pmc WRITE_SIZE as two separate passes (the counter
     budget of one pass, MI355X_MICROARCH.md) over a short child run of this bench
@@ -343,6 +395,7 @@ def live_traffic(args, batch, name_fragment, timeout=120):
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK",
                         "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    env = child_device_env(env, local_dev)   # at N > 1: only rank 0's GPU
     env["TMPDIR"] = "/tmp"
     kb = {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -388,7 +441,7 @@ def launch_check(args):
 def main(argv=None):
     raw = sys.argv[1:] if argv is None else argv
     args = parse(raw)
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+    if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.force_pg):
         # Launch N ranks; this process never touches a GPU (it only waits).
         sys.exit(subprocess.run(launch_command(raw, args.gpus)).returncode)
     if args.launch_check:
@@ -406,20 +459,24 @@ def main(argv=None):
     B = args.batch if args.batch else wl["hands"]
     gather = wl["gather"] if args.gather is None else args.gather
     with_trans = wl["trans"]
+    # The process-group path: every N > 1 run, and with --force-pg a 1-rank
+    # rehearsal of the same code (RCCL communicator, id broadcast, gather,
+    # device all_reduce, all_gather_object) on one GPU.
+    dist_on = world > 1 or args.force_pg
     # One process per GPU.  `--backend gloo` is a control-flow rehearsal mode
     # (several ranks may share one GPU); the real multi-GPU run uses RCCL.
     ndev = torch.cuda.device_count()
     local_dev = local if args.backend == "nccl" else local % max(ndev, 1)
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
-    if world > 1:
+    if dist_on:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
 
     from mano_amd import ManoHip, load_dump, synthetic_params
-    from mano_amd.distributed import AbiGather, gather_to_root
+    from mano_amd.distributed import AbiGather, all_gather, gather_to_root
     params = load_dump(args.model) if args.model else synthetic_params(0)
     model = ManoHip(params, device=local_dev, precision=args.precision)
 
@@ -429,55 +486,78 @@ def main(argv=None):
     verts = torch.empty((B, V, 3), device=dev)
     joints = torch.empty((B, 16, 3), device=dev)
     stream = torch.cuda.current_stream(dev)
-    out = {"verts": verts, "joints": joints}
     model.workspace(B)  # allocated before timing (covers every path)
     gatherer, gv, gj = None, None, None
-    if gather and world > 1:
+    gather_on = bool(gather and dist_on)
+    impl = args.gather_impl
+    if gather_on:
         if args.backend == "nccl":
             gatherer = AbiGather(local_dev)
-        if rank == 0:  # GPU 0's assembled buffers (mano_gather's layout), allocated once
+        if rank == 0 or impl == "allgather":
+            # the assembled buffers (rank r's rows at r*B), allocated once: GPU 0's
+            # (mano_gather), or every GPU's (mano_allgather)
             gv = torch.empty((B * world, V, 3), device=dev)
             gj = torch.empty((B * world, 16, 3), device=dev)
+
+    def do_gather(which):
+        if gatherer is not None:
+            if which == "allgather":   # RCCL ring, every rank gets the batch
+                gatherer.allgather(verts, out=gv)
+                gatherer.allgather(joints, out=gj)
+            else:                      # RCCL over xGMI, peer -> GPU 0 sends
+                gatherer.gather(verts, B * world, root=0, out=gv)
+                gatherer.gather(joints, B * world, root=0, out=gj)
+        else:  # gloo rehearsal: verts + joints through the host into the same gv / gj layout
+            if which == "allgather":
+                fv = all_gather(verts.cpu(), B * world)
+                fj = all_gather(joints.cpu(), B * world)
+            else:
+                fv = gather_to_root(verts.cpu(), B * world, root=0)
+                fj = gather_to_root(joints.cpu(), B * world, root=0)
+            if gv is not None:
+                gv.copy_(fv)
+                gj.copy_(fj)
 
     # Launch sequence of one step; `marks` get an event after each kernel.
     # "forward" issues exactly mano_forward's two launches (articulate, then
     # the fused blend GEMM + LBS) through the stage calls so that each kernel
     # is bracketed by events on its stream; "api" is one mano_forward call.
-    def run_path(path, marks=None):
+    # `dst` = (verts, joints) to write: the timed outputs, or the scratch
+    # pair of the untimed kernel table (so the timed step's outputs are what
+    # the correctness leg and the gathers read).
+    def run_path(path, marks=None, dst=None):
+        vo, jo = dst if dst is not None else (verts, joints)
+
         def mark(i):
             if marks is not None:
                 marks[i].record(stream)
         mark(0)
         if path == "forward":
-            model.stage_articulate(betas, pose, trans, joints=joints)
+            model.stage_articulate(betas, pose, trans, joints=jo)
             mark(1)
-            model.stage_blend_skin(B, verts, trans=trans)
+            model.stage_blend_skin(B, vo, trans=trans)
             mark(2)
         elif path == "api":
-            model.forward(betas, pose, trans, joints=True, out=out)
+            model.forward(betas, pose, trans, joints=True, out={"verts": vo, "joints": jo})
             mark(1)
         else:  # unfused: articulate, blend GEMM (v_posed to HBM), LBS
-            model.stage_articulate(betas, pose, trans, joints=joints)
+            model.stage_articulate(betas, pose, trans, joints=jo)
             mark(1)
             model.stage_blend(B)
             mark(2)
-            model.stage_skin(B, verts, trans=trans)
+            model.stage_skin(B, vo, trans=trans)
             mark(3)
 
     n_marks = {"forward": 3, "api": 2, "unfused": 4}
 
-    def step(marks=None):
+    def step(marks=None, gmarks=None):
         run_path(args.path, marks)
-        if gather and world > 1:
-            if gatherer is not None:  # RCCL over xGMI, peer -> GPU 0 sends
-                gatherer.gather(verts, B * world, root=0, out=gv)
-                gatherer.gather(joints, B * world, root=0, out=gj)
-            else:  # gloo rehearsal: verts + joints through the host into the same gv / gj layout
-                fv = gather_to_root(verts.cpu(), B * world, root=0)
-                fj = gather_to_root(joints.cpu(), B * world, root=0)
-                if rank == 0:
-                    gv.copy_(fv)
-                    gj.copy_(fj)
+        if gather_on:
+            if gmarks is not None:
+                gmarks[0].record(stream)
+            do_gather(impl)
+            if gmarks is not None:
+                gmarks[1].record(stream)
 
     # Clock ramp, then the untimed warmup.
     t_ramp = time.perf_counter()
@@ -502,20 +582,37 @@ def main(argv=None):
     every = max(1, min(args.event_every, args.steps // 5))  # at least 5 sampled steps
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(n_marks[args.path])]
               if i % every == 0 else None for i in range(args.steps)]
-    if world > 1:
+    # the gather of the same sampled steps, bracketed on the same stream
+    gevents = [[torch.cuda.Event(enable_timing=True) for _ in range(2)]
+               if gather_on and i % every == 0 else None for i in range(args.steps)]
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(events[i])
+        step(events[i], gevents[i])
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     dt = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         t = torch.tensor([dt], device=dev if args.backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    gather_info = None
+    if gather_on:
+        gms = [e[0].elapsed_time(e[1]) for e in gevents if e is not None]
+        gather_info = gather_stats(impl, world, B, float(np.mean(gms)))
+        gather_info["ms_min"] = float(np.min(gms))
+        gather_info["ms_max"] = float(np.max(gms))
+        gather_info["sampled_steps"] = len(gms)
+        gather_info["backend"] = args.backend
+        gather_info["form"] = ({"sendrecv": "mano_gather: one RCCL group of ncclSend (peers) / ncclRecv "
+                                            "(GPU 0), each peer over its own xGMI link",
+                                "allgather": "mano_allgather: RCCL ring ncclAllGather"}[impl]
+                               if gatherer is not None else "gloo rehearsal through the host")
+        gather_info["timing"] = ("HIP events on rank 0's launch stream around the gather (verts + "
+                                 "joints) of every sampled timed step, after that step's kernels")
 
     def span(a, b, evs):
         return float(np.mean([e[a].elapsed_time(e[b]) for e in evs]))
@@ -531,13 +628,15 @@ def main(argv=None):
     other = {"fp32": "f16x3", "f16x3": "fp32"}[args.precision]
     ms_other = {}
     if rank == 0 and not args.no_extra:
+        scratch = (torch.empty_like(verts), torch.empty_like(joints))
+
         def time_path(path, into, reps=50):
             evs = [[torch.cuda.Event(enable_timing=True) for _ in range(n_marks[path])]
                    for _ in range(reps)]
             for _ in range(reps):
-                run_path(path)
+                run_path(path, dst=scratch)
             for e in evs:
-                run_path(path, e)
+                run_path(path, e, dst=scratch)
             torch.cuda.synchronize()
             for k, (a, b) in timed[path].items():
                 into.setdefault(k, span(a, b, evs))
@@ -548,11 +647,11 @@ def main(argv=None):
         # launch, as rocprof's kernel average sees it); in the unfused path
         # it follows the blend GEMM's 612 MB of freshly written v_posed.
         for _ in range(20):
-            model.stage_skin(B, verts, trans=trans)
+            model.stage_skin(B, scratch[0], trans=trans)
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(50)]
         for e0, e1 in evs:
             e0.record(stream)
-            model.stage_skin(B, verts, trans=trans)
+            model.stage_skin(B, scratch[0], trans=trans)
             e1.record(stream)
         torch.cuda.synchronize()
         ms["skin_back_to_back"] = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
@@ -560,6 +659,41 @@ def main(argv=None):
         for path in ("forward", "unfused"):
             time_path(path, ms_other)
         model.set_precision(args.precision)
+        del scratch
+
+    # The other gather form (report both), timed after the
+    # timed region on every rank the same way; its buffers are freed after.
+    if gather_on and gatherer is not None and args.gather_compare_reps > 0:
+        other_impl = "allgather" if impl == "sendrecv" else "sendrecv"
+        keep = (gv, gj)
+        if other_impl == "allgather" or rank == 0:
+            gv = torch.empty((B * world, V, 3), device=dev)
+            gj = torch.empty((B * world, 16, 3), device=dev)
+        else:
+            gv = gj = None
+        do_gather(other_impl)   # untimed first call (RCCL sets up its channels)
+        torch.cuda.synchronize()
+        dist.barrier()
+        cev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)]
+               for _ in range(args.gather_compare_reps)]
+        for e in cev:
+            e[0].record(stream)
+            do_gather(other_impl)
+            e[1].record(stream)
+        torch.cuda.synchronize()
+        cms = [e[0].elapsed_time(e[1]) for e in cev]
+        cmp_info = gather_stats(other_impl, world, B, float(np.mean(cms)))
+        cmp_info.update({"ms_min": float(np.min(cms)), "ms_max": float(np.max(cms)), "reps": len(cms),
+                         "timing": "after the timed region, the gather alone back to back (no forward "
+                                   "in between), HIP events on rank 0's stream"})
+        if rank == 0:
+            chk = check_gather(model, wl["seed"], B, world, gv, gj, with_trans)
+            cmp_info["bit_exact"] = chk["bit_exact"]
+            cmp_info["hands_checked"] = chk["hands_checked"]
+        gather_info["compare"] = cmp_info
+        gv, gj = keep
+        torch.cuda.synchronize()
+        dist.barrier()
 
     def tflops(flop, t):
         return flop * B / (t * 1e-3) / 1e12
@@ -643,22 +777,6 @@ def main(argv=None):
         else:
             roof = {"kernel": kd["kernel"], "bound": "hbm", "achieved": kd["achieved_GBs"],
                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": kd["frac"]}
-        traffic, src, live = None, None, None
-        if rank == 0 and world == 1 and not args.no_live_pmc:
-            frag = PMC_KERNEL_NAME.get(dominant + ("_h3" if args.precision == "f16x3" else ""))
-            if frag is not None:
-                traffic, live = live_traffic(args, B, frag)
-                if traffic is not None:
-                    src = (f"measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over "
-                           f"a 3-step child run at {B} hands (read = 2 x FETCH_SIZE)")
-        if traffic is None:
-            traffic, src = load_traffic(args.pmc, dominant + ("_h3" if args.precision == "f16x3" else ""), B)
-            if live is not None:
-                src = f"{src} (live passes failed: {live})"
-        roof["traffic"] = traffic
-        roof["traffic_source"] = src
-        if isinstance(live, dict):
-            roof["traffic_detail"] = live
         roof["algorithmic_per_hand"] = kd.get("flop_per_hand", kd.get("bytes_per_hand"))
         roof["hands_per_launch"] = B
         roof["timed_in_region"] = dominant in in_path
@@ -675,11 +793,11 @@ def main(argv=None):
                                    args.model, with_trans)
         correctness["device_status"] = device_status
         correctness["pass"] = bool(correctness.get("pass")) and device_status == 0
-        if world > 1:
+        if dist_on:
             per_rank = [None] * world
             dist.all_gather_object(per_rank, correctness)
             correctness = merge_checks(per_rank)
-    elif world > 1:
+    elif dist_on:
         st = [None] * world
         dist.all_gather_object(st, device_status)
         device_status = max(st)
@@ -689,6 +807,46 @@ def main(argv=None):
         gather_check = check_gather(model, wl["seed"], B, world, gv, gj, with_trans)
         if args.dump_gather:
             np.savez(args.dump_gather, verts=gv.cpu().numpy(), joints=gj.cpu().numpy())
+
+    # Rank 0's host-side legs, at every N (the other ranks wait at a barrier,
+    # their GPUs idle): roofline.traffic by two rocprofv3 --pmc passes over a
+    # child run on rank 0's GPU only, the drop-in latency, the CPU baseline.
+    extra = {}
+    if rank == 0:
+        if roof is not None:
+            traffic, src, live = None, None, None
+            if not args.no_live_pmc:
+                frag = PMC_KERNEL_NAME.get(dominant + ("_h3" if args.precision == "f16x3" else ""))
+                if frag is not None:
+                    traffic, live = live_traffic(args, B, frag, local_dev=local_dev)
+                    if traffic is not None:
+                        src = (f"measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over "
+                               f"a 3-step 1-rank child run at {B} hands on rank 0's GPU (read = 2 x FETCH_SIZE)"
+                               + (" -- the kernel's per-launch bytes at this shard size; every rank's "
+                                  "launch is the same shape" if world > 1 else ""))
+            if traffic is None:
+                traffic, src = load_traffic(args.pmc, dominant + ("_h3" if args.precision == "f16x3" else ""), B)
+                if live is not None:
+                    src = f"{src} (live passes failed: {live})"
+            roof["traffic"] = traffic
+            roof["traffic_source"] = src
+            if isinstance(live, dict):
+                roof["traffic_detail"] = live
+        if not args.no_dropin:
+            extra["dropin"] = dropin_latency(params, local_dev)
+        if not args.no_cpu:
+            procs = args.cpu_procs or cpu_share(world)
+            cb = cpu_baseline(procs, args.cpu_seconds)
+            if world > 1:
+                cb["note"] = (f"rank 0 after the timed region while the other {world - 1} ranks wait at a "
+                              f"barrier; {procs} of this node's cores")
+            extra["cpu_baseline"] = cb
+            if "dropin" in extra and cb.get("value"):
+                # the per-hand port's time per hand on ONE core (the reference's
+                # own loop runs at 1/1.055 of it: profiles/cpu_calibration.json)
+                extra["dropin"]["cpu_port_us_per_hand_one_core"] = cb["cores"] / cb["value"] * 1e6
+    if dist_on:
+        dist.barrier()
 
     if rank == 0:
         total = B * world * args.steps
@@ -713,31 +871,28 @@ def main(argv=None):
             "config": {"workload": wl["desc"] if B == wl["hands"] else f"{args.workload} at {B} hands per GPU",
                        "hands_per_gpu": B, "global_batch": B * world,
                        "outputs": "verts+joints", "trans": with_trans, "path": args.path,
-                       "gather_to_gpu0": bool(gather and world > 1),
-                       "gather_impl": None if not (gather and world > 1) else
-                       ("mano_gather (RCCL send/recv)" if gatherer is not None else "gloo rehearsal"),
+                       "gather_to_gpu0": gather_on,
+                       "gather_impl": None if not gather_on else
+                       ({"sendrecv": "mano_gather (RCCL send/recv)", "allgather": "mano_allgather (RCCL ring)"}[impl]
+                        if gatherer is not None else "gloo rehearsal"),
                        "parallelism": f"dp{world}"},
+            "process_group": ({"backend": args.backend, "world": world, "forced_at_one_rank": world == 1}
+                              if dist_on else None),
             "roofline": roof,
             "kernels": kernels,
             "correctness": correctness,
             "device_status": device_status,
         }
+        if gather_info is not None:
+            line["gather"] = gather_info
         if gather_check is not None:
             line["gather_check"] = gather_check
-        if world == 1 and not args.no_dropin:
-            line["dropin"] = dropin_latency(params, local_dev)
-        if world == 1 and not args.no_cpu:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_procs or cpu_share(), args.cpu_seconds)
-            cb = line["cpu_baseline"]
-            if "dropin" in line and cb.get("value"):
-                # the per-hand port's time per hand on ONE core (the reference's
-                # own loop runs at 1/1.055 of it: profiles/cpu_calibration.json)
-                line["dropin"]["cpu_port_us_per_hand_one_core"] = cb["cores"] / cb["value"] * 1e6
+        line.update(extra)
         print(json.dumps(line), flush=True)
     if gatherer is not None:
         gatherer.close()
     model.close()
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

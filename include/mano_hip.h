@@ -97,8 +97,10 @@ int mano_model_info(const mano_model* model, int32_t* n_verts, int32_t* device);
 /* Device status word of a model: MANO_DEVICE_* bits raised by kernels since
  * the last clear.  Waits for every launch on the model's device first
  * (hipDeviceSynchronize), reads the word into *status and, with `clear`
- * non-zero, resets it.  A non-zero word means some launch's outputs are not
- * valid:
+ * non-zero, resets it -- the read and the reset are one device atomic, so a
+ * bit raised by a launch from another thread is reported by this call or by
+ * the next, never dropped.  A non-zero word means some launch's outputs are
+ * not valid:
  *   MANO_DEVICE_SKIN_HANDOFF_TIMEOUT  the standalone LBS (mano_stage_skin) lost
  *     a hand-over between its memory and compute waves (a bounded LDS wait
  *     gave up); the verts of the units it could not confirm were not
@@ -237,11 +239,19 @@ int mano_comm_create(int device, int32_t n_ranks, int32_t rank, const unsigned c
 int mano_comm_destroy(mano_comm* comm);
 int mano_gather(mano_comm* comm, const void* send, size_t send_bytes, void* recv,
                 const size_t* rank_bytes, int32_t root, void* stream);
+/* Every rank receives every shard: RCCL's ring ncclAllGather of equal
+ * `send_bytes` shards, rank r's bytes at recv + r * send_bytes on EVERY rank
+ * (recv holds n_ranks * send_bytes).  The comparison form for mano_gather
+ * (a ring is bound by one link per hop), and the call for
+ * callers that want the whole batch on every device.  Asynchronous on
+ * `stream`. */
+int mano_allgather(mano_comm* comm, const void* send, size_t send_bytes, void* recv,
+                   void* stream);
 
 /* Message of the last failed call on this thread ("" if none). */
 const char* mano_last_error(void);
 
-/* ABI version, bumped on any signature change. */
+/* ABI version, bumped on any signature change (4: + mano_allgather). */
 int mano_abi_version(void);
 
 #ifdef __cplusplus

@@ -94,7 +94,7 @@ int set_error(int code, const char* msg) {
 
 extern "C" {
 
-int mano_abi_version(void) { return 3; }
+int mano_abi_version(void) { return 4; }
 
 const char* mano_last_error(void) { return g_last_error.c_str(); }
 
@@ -146,7 +146,7 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   parts[kPcaB] = {hm.pca.data(), hm.pca.size() * 4, 0};
   parts[kPcaM] = {hm.pmean.data(), hm.pmean.size() * 4, 0};
   parts[kZeros] = {zeros.data(), zeros.size() * 4, 0};
-  parts[kStatus] = {zeros.data(), 4, 0};
+  parts[kStatus] = {zeros.data(), 8, 0};  // [0] the status word, [1] its snapshot (device_status)
   parts[kBasis16] = {hm.b16.data(), hm.b16.size() * 4, 0};
   parts[kW16] = {hm.w16.data(), hm.w16.size() * 4, 0};
   parts[kBasisH3] = {hm.bh3.data(), hm.bh3.size() * 2, 0};
@@ -237,6 +237,24 @@ int mano_model_get_precision(const mano_model* m, int32_t* precision) {
   return MANO_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// mano_model_device_status's read (and clear) of the status word as ONE
+// device atomic, so a bit a kernel on another stream or thread raises
+// between the read and the clear is never lost: it lands either in the
+// snapshot or, after the exchange, in the word for the next call.
+__global__ void status_take_kernel(int32_t* word, int32_t clear) {
+  if (threadIdx.x == 0) {
+    int32_t v = clear ? __hip_atomic_exchange(word, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    word[1] = v;  // plain vector store of the snapshot
+  }
+}
+}  // namespace
+
+extern "C" {
+
 int mano_model_device_status(const mano_model* m, int32_t* status, int32_t clear) {
   g_last_error.clear();
   if (int rc = check_model(m)) return rc;
@@ -245,14 +263,12 @@ int mano_model_device_status(const mano_model* m, int32_t* status, int32_t clear
   if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
   hipError_t e = hipDeviceSynchronize();
   if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
+  hipLaunchKernelGGL(status_take_kernel, dim3(1), dim3(64), 0, nullptr, m->dm.status, clear ? 1 : 0);
+  e = hipGetLastError();
+  if (e != hipSuccess) return hip_fail(e, "status_take_kernel launch");
   int32_t word = 0;
-  e = hipMemcpy(&word, m->dm.status, sizeof(word), hipMemcpyDeviceToHost);
+  e = hipMemcpy(&word, m->dm.status + 1, sizeof(word), hipMemcpyDeviceToHost);  // after the kernel (null stream)
   if (e != hipSuccess) return hip_fail(e, "hipMemcpy(status)");
-  if (clear && word != 0) {
-    e = hipMemset(m->dm.status, 0, sizeof(word));
-    if (e == hipSuccess) e = hipDeviceSynchronize();
-    if (e != hipSuccess) return hip_fail(e, "hipMemset(status)");
-  }
   *status = word;
   return MANO_OK;
 }

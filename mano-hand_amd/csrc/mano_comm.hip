@@ -65,6 +65,7 @@ struct Rccl {
   decltype(&ncclRecv) recv = nullptr;
   decltype(&ncclGroupStart) group_start = nullptr;
   decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
 };
 
@@ -90,6 +91,7 @@ const Rccl& rccl() {
     r.recv = reinterpret_cast<decltype(r.recv)>(sym("ncclRecv"));
     r.group_start = reinterpret_cast<decltype(r.group_start)>(sym("ncclGroupStart"));
     r.group_end = reinterpret_cast<decltype(r.group_end)>(sym("ncclGroupEnd"));
+    r.all_gather = reinterpret_cast<decltype(r.all_gather)>(sym("ncclAllGather"));
     r.error_string = reinterpret_cast<decltype(r.error_string)>(sym("ncclGetErrorString"));
     r.ok = r.why.empty();
   });
@@ -218,6 +220,24 @@ int mano_gather(mano_comm* c, const void* send, size_t send_bytes, void* recv,
   const ncclResult_t end = r.group_end();
   if (res != ncclSuccess) return rccl_fail(r, res, is_root ? "ncclRecv" : "ncclSend");
   if (end != ncclSuccess) return rccl_fail(r, end, "ncclGroupEnd");
+  return MANO_OK;
+}
+
+int mano_allgather(mano_comm* c, const void* send, size_t send_bytes, void* recv, void* stream) {
+  mano::set_error(MANO_OK, "");
+  if (int rc = check_comm(c)) return rc;
+  if (send_bytes == 0) return MANO_OK;
+  if (!send) return fail(MANO_EINVAL, "send is NULL");
+  if (!recv) return fail(MANO_EINVAL, "recv is NULL");
+  const Rccl& r = rccl();
+  DeviceGuard guard(c->device);
+  if (guard.err != hipSuccess)
+    return fail(MANO_EHIP, "hipSetDevice: %s", hipGetErrorString(guard.err));
+  // RCCL's ring all-gather: each of the n - 1 steps forwards one shard to the
+  // next rank, so every shard crosses n - 1 links in turn.
+  ncclResult_t res = r.all_gather(send, recv, send_bytes, ncclChar, c->comm,
+                                  static_cast<hipStream_t>(stream));
+  if (res != ncclSuccess) return rccl_fail(r, res, "ncclAllGather");
   return MANO_OK;
 }
 

@@ -389,7 +389,9 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
   // first tile chain (after K-group 2), so the 8 stores of a group do not
   // issue as one burst (0.605 vs 0.619 ms, same box; the verts-only kernel
   // spills under the extra live registers and keeps its stores together).
-  constexpr bool kDefer = kVposed;
+  // (Diagnostic ablation builds store nothing or store elsewhere: no deferral,
+  // so `pend` / `poff` are never flushed unassigned.)
+  constexpr bool kDefer = kVposed && MANO_BS_ABLATE == 0;
   // nontemporal only with one output stream (beside the rest_verts stream
   // either one nontemporal took 0.71 vs 0.61 ms, both 0.86:
   // profiles/r03m_ab_rest_nt.jsonl)

@@ -87,6 +87,7 @@ SIGNATURES = {
     "mano_comm_create": (ctypes.c_int, [ctypes.c_int, _i32, _i32, ctypes.c_char_p, ctypes.POINTER(_p)]),
     "mano_comm_destroy": (ctypes.c_int, [_p]),
     "mano_gather": (ctypes.c_int, [_p, _p, ctypes.c_size_t, _p, ctypes.POINTER(ctypes.c_size_t), _i32, _p]),
+    "mano_allgather": (ctypes.c_int, [_p, _p, ctypes.c_size_t, _p, _p]),
 }
 
 _LIB = None

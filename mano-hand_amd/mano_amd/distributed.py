@@ -91,7 +91,7 @@ class AbiGather:
         uid = ctypes.create_string_buffer(_abi.MANO_COMM_ID_BYTES)
         if rank == 0:
             _abi.check(lib.mano_comm_unique_id(uid))
-        if world > 1:
+        if dist.is_available() and dist.is_initialized():  # also a 1-rank group (bench --force-pg)
             box = [uid.raw]
             dist.broadcast_object_list(box, src=0 if group is None else dist.get_global_rank(group, 0),
                                        group=group)
@@ -122,6 +122,25 @@ class AbiGather:
             None if full is None else ctypes.c_void_p(full.data_ptr()), sizes, root,
             ctypes.c_void_p(s.cuda_stream)))
         return full
+
+    def allgather(self, shard: torch.Tensor, out: Optional[torch.Tensor] = None,
+                  stream=None) -> torch.Tensor:
+        """Every rank gets the (world * rows, ...) concatenation of all shards
+        (RCCL's ring all-gather, mano_allgather; equal shards only) -- the
+        comparison form for `gather`."""
+        if not shard.is_contiguous():
+            raise ValueError("shard must be contiguous")
+        shape = (self.world * shard.shape[0],) + tuple(shard.shape[1:])
+        s = stream if stream is not None else torch.cuda.current_stream(shard.device)
+        if out is None:
+            with torch.cuda.stream(s):
+                out = torch.empty(shape, dtype=shard.dtype, device=shard.device)
+        elif tuple(out.shape) != shape or not out.is_contiguous() or out.dtype != shard.dtype:
+            raise ValueError(f"out must be contiguous {shard.dtype} of shape {shape}")
+        _abi.check(_abi.lib().mano_allgather(
+            self._c, ctypes.c_void_p(shard.data_ptr()), shard.numel() * shard.element_size(),
+            ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(s.cuda_stream)))
+        return out
 
     def close(self):
         if getattr(self, "_c", None) is not None and self._c.value:

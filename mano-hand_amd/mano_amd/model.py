@@ -126,6 +126,9 @@ class ManoHip:
     def workspace_bytes(self, n: int) -> int:
         return int(_abi.lib().mano_workspace_bytes(self._h, n))
 
+    def forward_workspace_bytes(self, n: int) -> int:
+        return int(_abi.lib().mano_forward_workspace_bytes(self._h, n))
+
     def workspace_offsets(self, n: int):
         a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
         _abi.check(_abi.lib().mano_workspace_offsets(self._h, n, ctypes.byref(a), ctypes.byref(b),
@@ -167,8 +170,20 @@ class ManoHip:
         base = ws.data_ptr()
         return ws[((base + 255) & ~255) - base:]
 
-    def _ws_args(self, n, forward_only: bool = False, stream=None):
-        ws = self.workspace(n, forward_only, stream)
+    def _ws_args(self, n, forward_only: bool = False, stream=None, workspace=None):
+        if workspace is not None:
+            # the caller's own workspace (e.g. one a captured HIP graph holds),
+            # never one of the per-stream entries above
+            need = int(_abi.lib().mano_forward_workspace_bytes(self._h, n) if forward_only
+                       else _abi.lib().mano_workspace_bytes(self._h, n))
+            if (not isinstance(workspace, torch.Tensor) or workspace.device != self.device
+                    or workspace.dtype != torch.uint8 or not workspace.is_contiguous()):
+                raise ValueError(f"workspace must be a contiguous uint8 tensor on {self.device}")
+            if workspace.numel() < need + 256:
+                raise ValueError(f"workspace has {workspace.numel()} bytes, {need + 256} needed for {n} hands")
+            ws = workspace
+        else:
+            ws = self.workspace(n, forward_only, stream)
         base = ws.data_ptr()
         aligned = (base + 255) & ~255
         return ctypes.c_void_p(aligned), ctypes.c_size_t(ws.numel() - (aligned - base))
@@ -221,13 +236,15 @@ class ManoHip:
     def forward(self, betas: torch.Tensor, pose: torch.Tensor, trans: Optional[torch.Tensor] = None,
                 *, joints: bool = True, rest_verts: bool = False, rest_joints: bool = False,
                 rot_mats: bool = False, out: Optional[Dict[str, torch.Tensor]] = None,
-                stream=None) -> Dict[str, torch.Tensor]:
+                stream=None, workspace: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
         """Batched MANOModel.update() (mano_np.py:79-115) on the GPU.
 
         betas (B,10) or (10,) shared, pose (B,16,3) or (B,48) axis-angle,
         trans (B,3) optional.  Returns float32 device tensors: verts (B,V,3),
         and on request joints (B,16,3) posed, rest_verts (B,V,3),
-        rest_joints (B,16,3), rot_mats (B,16,3,3).
+        rest_joints (B,16,3), rot_mats (B,16,3,3).  `workspace`: a uint8
+        device tensor of at least forward_workspace_bytes(B) + 256 bytes that
+        the caller owns (default: the engine's per-stream workspace).
         """
         B, betas, bstride, pose, trans = self._inputs(betas, pose, trans)
         V = self.n_verts
@@ -236,7 +253,7 @@ class ManoHip:
             ("rest_verts", (B, V, 3), rest_verts), ("rest_joints", (B, N_JOINTS, 3), rest_joints),
             ("rot_mats", (B, N_JOINTS, 3, 3), rot_mats)))
         g = lambda k: _ptr(res.get(k))  # noqa: E731
-        ws, wsb = self._ws_args(B, forward_only=True, stream=stream)
+        ws, wsb = self._ws_args(B, forward_only=True, stream=stream, workspace=workspace)
         _abi.check(_abi.lib().mano_forward(
             self._h, B, _ptr(betas), bstride, _ptr(pose), _ptr(trans), g("verts"),
             g("joints") if joints else None, g("rest_verts") if rest_verts else None,
@@ -503,7 +520,13 @@ class MANOModel:
 
             d_in, h_in, v_in = carve(self._IN, self.device, True)
             d_out, h_out, v_out = carve(outs, self.device, True)
-            self._io = (d_in, h_in, v_in, d_out, h_out, v_out)
+            # the batch-1 forward's own workspace: the eager calls and every
+            # captured graph use it (a graph holds its raw pointer), and it is
+            # never one of the engine's per-stream workspaces, which another
+            # call on a pooled stream of the same handle could regrow and free
+            ws = torch.empty(self.engine.forward_workspace_bytes(1) + 256, dtype=torch.uint8,
+                             device=self.device)
+            self._io = (d_in, h_in, v_in, d_out, h_out, v_out, ws)
         return self._io
 
     def update(self):
@@ -514,7 +537,7 @@ class MANOModel:
         shape = np.asarray(self.shape, dtype=np.float64)
         if shape.shape != (self.n_shape_params,):
             raise ValueError(f"shape has shape {shape.shape}, ({self.n_shape_params},) expected")
-        d_in, h_in, v_in, d_out, h_out, v_out = self._io_buffers()
+        d_in, h_in, v_in, d_out, h_out, v_out, _ = self._io_buffers()
         # float64 -> float32 exactly as np.asarray(..., dtype=np.float32) would
         v_in["shape"][1][...] = shape
         v_in["pose"][1][...] = pose.reshape(self.n_joints, 3)
@@ -538,18 +561,19 @@ class MANOModel:
     def _update_body(self, with_trans):
         """H2D of the packed inputs, mano_forward, D2H of the packed outputs
         (on the current stream; no sync)."""
-        d_in, h_in, v_in, d_out, h_out, v_out = self._io_buffers()
+        d_in, h_in, v_in, d_out, h_out, v_out, ws = self._io_buffers()
         d_in.copy_(h_in, non_blocking=True)
         self.engine.forward(v_in["shape"][0], v_in["pose"][0], v_in["trans"][0] if with_trans else None,
                             joints=True, rest_verts=True, rest_joints=True, rot_mats=True,
-                            out={k: dv for k, (dv, _) in v_out.items()})
+                            out={k: dv for k, (dv, _) in v_out.items()}, workspace=ws)
         h_out.copy_(d_out, non_blocking=True)
 
     def _graph(self, key):
         """The update body captured into a HIP graph (one per translation
-        mode and engine precision), built on first use: an eager run on the
-        capture stream first (it allocates that stream's workspace outside the
-        capture)."""
+        mode and engine precision), built on first use after an eager run on
+        the capture stream.  The graph reads and writes only this object's
+        packed I/O blocks and its private batch-1 workspace (`_io_buffers`),
+        which live as long as the object."""
         with_trans = key[0]
         if key not in self._graphs:
             g = None
@@ -566,9 +590,9 @@ class MANOModel:
             except RuntimeError:
                 g = None  # capture refused: keep the eager launches (same kernels)
             cur.wait_stream(side)
-            # the graph holds raw pointers into `side`'s workspace: keep the
-            # stream (and so its workspace entry, batch 1, never regrown) alive
-            self._graphs[key] = (g, side)
+            # the graph holds raw pointers into the private workspace and the
+            # I/O blocks; keep them referenced beside it
+            self._graphs[key] = (g, side, self._io)
         return self._graphs[key][0]
 
     def forward_batch(self, betas, pose, trans=None, **kw):

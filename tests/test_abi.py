@@ -17,7 +17,7 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, n), n
         assert n in _abi.SIGNATURES, f"{n} declared in the header but not bound"
     assert set(_abi.SIGNATURES) == set(names)
-    assert lib.mano_abi_version() == 3
+    assert lib.mano_abi_version() == 4
 
 
 @pytest.mark.parametrize("cc,lang", [("g++", "c++"), ("gcc", "c")])
@@ -106,6 +106,7 @@ def test_forward_pca_and_comm_argument_checks():
     assert lib.mano_comm_create(0, 1, 0, None, ctypes.byref(out)) == _abi.MANO_EINVAL
     assert lib.mano_comm_destroy(None) == _abi.MANO_OK
     assert lib.mano_gather(None, None, 0, None, None, 0, None) == _abi.MANO_EINVAL
+    assert lib.mano_allgather(None, None, 0, None, None) == _abi.MANO_EINVAL
     assert lib.mano_comm_unique_id(None) == _abi.MANO_EINVAL
 
 

@@ -72,6 +72,39 @@ def test_traffic_lookup(tmp_path):
 
 def test_cpu_share_bounded():
     assert 1 <= bench.cpu_share() <= 16
+    assert bench.cpu_share() <= bench.cpu_share(8) <= 128
+
+
+def test_gather_stats():
+    """The C4 line's gather figures: bytes into GPU 0 and per-link rates of the
+    two forms (send/recv: one shard per peer link; ring: world - 1 shards per
+    link)."""
+    B, w = 524288, 8
+    shard = B * 9528
+    g = bench.gather_stats("sendrecv", w, B, 40.0)
+    assert g["shard_bytes"] == shard and g["bytes_to_gpu0"] == 7 * shard and g["links"] == 7
+    assert g["GBs_to_gpu0"] == pytest.approx(7 * shard / 0.040 / 1e9)
+    assert g["link_GBs"] == pytest.approx(shard / 0.040 / 1e9)
+    assert g["link_frac"] == pytest.approx(g["link_GBs"] / 153.0)
+    a = bench.gather_stats("allgather", w, B, 200.0)
+    assert a["links"] == 8 and a["bytes_landed_total"] == 8 * 7 * shard
+    assert a["link_GBs"] == pytest.approx(7 * shard / 0.2 / 1e9)
+    one = bench.gather_stats("sendrecv", 1, 4096, 0.1)
+    assert one["bytes_to_gpu0"] == 0 and one["link_frac"] is None
+
+
+def test_child_device_env():
+    """The --pmc child at N > 1 sees only rank 0's GPU."""
+    assert bench.child_device_env({}, 3)["HIP_VISIBLE_DEVICES"] == "3"
+    assert bench.child_device_env({"HIP_VISIBLE_DEVICES": "4,5,6"}, 1)["HIP_VISIBLE_DEVICES"] == "5"
+    e = bench.child_device_env({"CUDA_VISIBLE_DEVICES": "2,7"}, 1)
+    assert e["CUDA_VISIBLE_DEVICES"] == "7" and "HIP_VISIBLE_DEVICES" not in e
+
+
+def test_force_pg_and_gather_flags():
+    a = bench.parse(["--force-pg", "--gather-impl", "allgather", "--workload", "C4"])
+    assert a.force_pg and a.gather_impl == "allgather" and a.gather_compare_reps > 0
+    assert bench.parse([]).gather_impl == "sendrecv" and not bench.parse([]).force_pg
 
 
 def test_pmc_values_parse(tmp_path):

@@ -94,14 +94,26 @@ def test_bench_c4_gather_rehearsal_layout(tmp_path):
     dump = tmp_path / "gather.npz"
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(world), "--backend", "gloo",
-                        "--workload", "C4", "--batch", str(B), "--steps", "3", "--warmup", "1",
-                        "--ramp-seconds", "0", "--no-cpu", "--no-extra", "--no-live-pmc",
-                        "--dump-gather", str(dump)], capture_output=True, text=True, timeout=300, env=env)
+                        "--workload", "C4", "--batch", str(B), "--steps", "5", "--warmup", "1",
+                        "--ramp-seconds", "0", "--cpu-seconds", "1", "--cpu-procs", "2", "--no-extra",
+                        "--no-dropin", "--dump-gather", str(dump)],
+                       capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert line["n_gpus"] == world and line["config"]["gather_to_gpu0"]
     assert line["gather_check"]["bit_exact"] and line["gather_check"]["hands_checked"] > 0
     assert line["correctness"]["pass"], line["correctness"]
+    assert line["correctness"]["ranks_checked"] == world
+    # the N > 1 line's own measurements: the gather timed on GPU 0, the CPU
+    # baseline on rank 0 while rank 1 waits, live HBM traffic of rank 0's kernel
+    g = line["gather"]
+    assert g["ms"] > 0 and g["sampled_steps"] >= 5 and g["bytes_to_gpu0"] == B * 9528
+    assert g["GBs_to_gpu0"] > 0 and g["link_frac"] is not None
+    assert line["cpu_baseline"]["value"] > 0 and line["cpu_baseline"]["cores"] == 2
+    assert "note" in line["cpu_baseline"]
+    assert line["roofline"]["traffic"] > 0, line["roofline"].get("traffic_source")
+    assert line["roofline"]["traffic_source"].startswith("measured in this run")
+    assert line["process_group"]["backend"] == "gloo" and line["process_group"]["world"] == world
     with np.load(dump) as z:
         gv, gj = z["verts"], z["joints"]
     from mano_amd import ManoHip, synthetic_params
@@ -113,3 +125,43 @@ def test_bench_c4_gather_rehearsal_layout(tmp_path):
     assert np.array_equal(gv, out["verts"].cpu().numpy())
     assert np.array_equal(gj, out["joints"].cpu().numpy())
     m.close()
+
+
+@pytest.mark.parametrize("impl", ["sendrecv", "allgather"])
+def test_bench_one_rank_nccl_process_group(impl):
+    """The RCCL form of the N > 1 code, on one GPU: bench.py under torchrun
+    with one rank on the nccl backend and --force-pg runs
+    init_process_group("nccl", device_id), AbiGather's id broadcast
+    (broadcast_object_list) -> mano_comm_create, the timed gather
+    (mano_gather or mano_allgather) with its events, the on-device all_reduce
+    of the step time, all_gather_object of the correctness legs, the other
+    gather form as the comparison leg (RCCL's ring all-gather runs even at one
+    rank), and gather_check on GPU 0's assembled buffers."""
+    import json
+    import subprocess
+    B = 4096
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--force-pg", "--backend", "nccl",
+           "--workload", "C4", "--batch", str(B), "--steps", "10", "--warmup", "2", "--ramp-seconds", "0",
+           "--gather-impl", impl, "--no-extra", "--no-dropin"]
+    if impl == "sendrecv":   # the rank-0 legs of an N > 1 line, through the process-group path
+        cmd += ["--cpu-seconds", "1", "--cpu-procs", "2"]
+    else:
+        cmd += ["--no-cpu", "--no-live-pmc"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["process_group"] == {"backend": "nccl", "world": 1, "forced_at_one_rank": True}
+    assert line["config"]["gather_to_gpu0"] and line["n_gpus"] == 1
+    assert line["config"]["gather_impl"].startswith({"sendrecv": "mano_gather", "allgather": "mano_allgather"}[impl])
+    assert line["gather_check"]["bit_exact"], line["gather_check"]
+    assert line["correctness"]["pass"] and line["correctness"]["ranks_checked"] == 1, line["correctness"]
+    g = line["gather"]
+    assert g["impl"] == impl and g["ms"] > 0 and g["bytes_to_gpu0"] == 0
+    c = g["compare"]
+    assert c["impl"] == ("allgather" if impl == "sendrecv" else "sendrecv")
+    assert c["ms"] > 0 and c["reps"] >= 1 and c["bit_exact"]
+    if impl == "sendrecv":
+        assert line["cpu_baseline"]["value"] > 0
+        assert line["roofline"]["traffic"] > 0
+        assert line["roofline"]["traffic_source"].startswith("measured in this run")
