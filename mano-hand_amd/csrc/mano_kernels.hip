@@ -304,8 +304,9 @@ __device__ __forceinline__ void prio_down() {
 // (a never-taken data-dependent store keeps the work alive), 2 = no LBS
 // (v_posed is stored as verts), 3 = both, 4 = the same stores into a
 // line-aligned scratch layout (each 192-B hand segment at a 256-B boundary:
-// same instructions and bytes, no partially written lines; the verts buffer
-// must hold n * n_groups * 256 B).
+// same instructions, bytes, cache policy and deferral, no partially written
+// sector; the verts and rest_verts buffers must hold n * n_groups * 256 B,
+// tools/debug/align_bound.py reads them back in the reference layout).
 #ifndef MANO_BS_ABLATE
 #define MANO_BS_ABLATE 0
 #endif
@@ -391,7 +392,7 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
   // spills under the extra live registers and keeps its stores together).
   // (Diagnostic ablation builds store nothing or store elsewhere: no deferral,
   // so `pend` / `poff` are never flushed unassigned.)
-  constexpr bool kDefer = kVposed && MANO_BS_ABLATE == 0;
+  constexpr bool kDefer = kVposed && (MANO_BS_ABLATE == 0 || MANO_BS_ABLATE == 4);
   // nontemporal only with one output stream (beside the rest_verts stream
   // either one nontemporal took 0.71 vs 0.61 ms, both 0.86:
   // profiles/r03m_ab_rest_nt.jsonl)
@@ -475,8 +476,10 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
 #pragma unroll
         for (int c = 0; c < 3; ++c) tv[r][c] = trans[(h0 + min(row0 + r, n_valid - 1)) * 3 + c];
     }
-    float* vtile = verts + h0 * int64_t(vstride32);
-    float* ptile = kVposed ? vposed + h0 * int64_t(vstride32) : nullptr;
+    // ABLATE 4: tiles of 16 rows x n_groups x 64 floats (the aligned scratch layout)
+    const int64_t tile_floats = MANO_BS_ABLATE == 4 ? int64_t(n_groups) * 64 : int64_t(vstride32);
+    float* vtile = verts + h0 * tile_floats;
+    float* ptile = kVposed ? vposed + h0 * tile_floats : nullptr;
 
     // The W fragment rides in the slot of the group's first tile (LDS-DMA by
     // wave 2, which has the fewest basis pieces): a global load in the loop
@@ -541,12 +544,17 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
       int vb = grp * 16;
       if (vb > n_verts - 16) vb = n_verts - 16;
       const int voff = 3 * (vb + col);
+      // byte offset of row hr's point of this lane from the tile base
+      auto row_off = [&](int hr) -> unsigned {
+        if constexpr (MANO_BS_ABLATE == 4) return 4u * unsigned((hr * n_groups + grp) * 64 + 3 * col);
+        else return 4u * unsigned(hr * vstride32 + voff);
+      };
       if constexpr (kVposed) {
         // rest_verts leave before the LBS: their stores drain under its MFMAs
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int hr = min(row0 + r, n_valid - 1);
-          store_out<kRestNt>(byte_at(ptile, 4u * unsigned(hr * vstride32 + voff)), f32x3{p[0][r], p[1][r], p[2][r]});
+          store_out<kRestNt>(byte_at(ptile, row_off(hr)), f32x3{p[0][r], p[1][r], p[2][r]});
         }
       }
       f32x4 out[3];
@@ -578,11 +586,9 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
         // the SGPR-base + VGPR-offset store form, no 64-bit address VALU.
         // (opaque: hipcc otherwise hoists the row offsets and spills 10 VGPRs
         // in the verts-only range prologue)
-        unsigned boff = 4u * unsigned(hr * vstride32 + voff);
+        unsigned boff = row_off(hr);
         asm volatile("" : "+v"(boff));
-        if constexpr (MANO_BS_ABLATE == 4)  // needs a verts buffer of n * 49 * 256 B
-          *reinterpret_cast<f32x3*>(verts + ((h0 + hr) * n_groups + grp) * 64 + 3 * col) = f32x3{o0, o1, o2};
-        else if constexpr (kDefer) {
+        if constexpr (kDefer) {
           pend[r] = f32x3{o0, o1, o2};
           poff[r] = boff;
         } else

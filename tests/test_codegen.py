@@ -56,6 +56,31 @@ def test_skin_pair_vmcnt_protocol(report):
         assert r["waits"] >= 1 and r["ok"], (name, r)
 
 
+def test_no_repeated_store_data(report):
+    """tools/isa_scan.py rule 3: no run of stores of one unchanged data
+    register (the ext_vector bit_cast pitfall's shape) in any kernel."""
+    assert report["repeated_store_data"] == {}, report["repeated_store_data"]
+
+
+def test_repeated_store_rule_catches_the_bitcast_pitfall(tmp_path):
+    """The rule on a two-kernel fixture compiled here: the pitfall form
+    (__builtin_bit_cast of an ext_vector element: element 0 stored for every
+    row) is flagged, the product's form (a scalar copy first) is not."""
+    import subprocess
+    hipcc = "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not installed")
+    out = tmp_path / "pitfall.s"
+    r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "--cuda-device-only", "-S", "-o", str(out),
+                        os.path.join(REPO, "tests", "native", "bitcast_pitfall.hip")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    isa_scan = _tools()
+    flagged = isa_scan.scan_repeated_stores(out.read_text())
+    assert any("bug_kernel" in k for k in flagged), flagged
+    assert not any("ok_kernel" in k for k in flagged), flagged
+
+
 def _tools():
     import sys
     p = os.path.join(REPO, "tools")

@@ -1,4 +1,5 @@
-"""The code object the GPU tests run: no packed fp32 VALU, and skin_pair's
+"""The code object the GPU tests run: no packed fp32 VALU, no repeated store
+data, and skin_pair's
 hand-counted vmcnt protocol intact (tools/isa_scan.py).
 
 The disassembly is taken when this module is imported -- at collection,
@@ -60,3 +61,10 @@ def test_skin_pair_vmcnt_protocol_in_loaded_library():
     assert len(pairs) == 4
     for name, r in pairs.items():
         assert r["ok"], (name, r)
+
+
+def test_no_repeated_store_data_in_loaded_library():
+    """isa_scan rule 3 (the ext_vector bit_cast pitfall's shape) on the
+    library the GPU tests map."""
+    assert _REPORT is not None, _ERR
+    assert _REPORT["repeated_store_data"] == {}, _REPORT["repeated_store_data"]

@@ -35,11 +35,13 @@ def main(lib=LIB):
         "counts": {k: len(rx.findall(asm)) for k, rx in WATCH.items()},
         "examples": {k: [l.strip() for l in asm.splitlines() if rx.search(l)][:5] for k, rx in WATCH.items()},
         "skin_pair_vmcnt": scan["skin_pair_vmcnt"],
+        "repeated_store_data": scan["repeated_store_data"],
     }
     with open(lib + ".codegen.json", "w") as f:
         json.dump(report, f, indent=1)
     print(json.dumps({k: report[k] for k in ("mfma", "counts")} |
-                     {"skin_pair_vmcnt_ok": all(v["ok"] for v in scan["skin_pair_vmcnt"].values())}))
+                     {"skin_pair_vmcnt_ok": all(v["ok"] for v in scan["skin_pair_vmcnt"].values()),
+                      "repeated_store_data": len(scan["repeated_store_data"])}))
 
 
 if __name__ == "__main__":

@@ -16,6 +16,14 @@
    these ops fails here, on the CPU, instead of racing on the GPU.
    (`s_cbranch_execz` is taken as not taken: every exec-masked DMA of the
    memory wave keeps lane 0 active.)
+3. No repeated store data: a run of 4 or more vector-memory stores of the
+   same data register(s) with no write to them in between is flagged.  The
+   toolchain pitfall of round 3 (`__builtin_bit_cast(unsigned, v[r])` of an
+   `ext_vector_type` element compiles to element 0 for every r: sixteen
+   `buffer_store_dword v0, ...` at different offsets) has this
+   shape; storing one value to many places is nowhere in the design.
+   (tests/native/bitcast_pitfall.hip is a two-kernel fixture: the pitfall and
+   its fix; tests/test_codegen.py checks that the rule tells them apart.)
 
 Used by tools/codegen_report.py at build time and by tests/test_gpu_codegen.py
 on the library the GPU tests load (run in a child process started before the
@@ -151,6 +159,86 @@ def check_vmcnt_protocol(insts, n_dma, n_wait):
     return len(waits), failures
 
 
+_VREG = re.compile(r"^(?:v(\d+)|v\[(\d+):(\d+)\]|a(\d+)|a\[(\d+):(\d+)\])$")
+
+
+def _regs(op):
+    """VGPR / AGPR numbers named by one operand ('v5', 'v[4:7]', 'a3'), else ()."""
+    m = _VREG.match(op.strip())
+    if not m:
+        return ()
+    if m.group(1):
+        return (("v", int(m.group(1))),)
+    if m.group(2):
+        return tuple(("v", r) for r in range(int(m.group(2)), int(m.group(3)) + 1))
+    if m.group(4):
+        return (("a", int(m.group(4))),)
+    return tuple(("a", r) for r in range(int(m.group(5)), int(m.group(6)) + 1))
+
+
+def _store_data(mn, ops):
+    """Data registers of a vector-memory store (buffer_store: first operand;
+    global / flat / scratch_store: second), else None."""
+    if not re.match(r"(buffer|global|flat|scratch)_store", mn):
+        return None
+    parts = [p.strip() for p in ops.split(",")]
+    k = 0 if mn.startswith("buffer_") else 1
+    return _regs(parts[k]) if len(parts) > k else None
+
+
+def repeated_store_data(insts, min_run=4):
+    """Rule 3 over one function's [(mnemonic, operands)] in program order:
+    [(data registers, count)] for each run of >= min_run stores of the same
+    data registers with no instruction writing any of them in between."""
+    live, hits = {}, []
+    for mn, ops in insts:
+        data = _store_data(mn, ops)
+        if data:
+            live[data] = live.get(data, 0) + 1
+            if live[data] == min_run:
+                hits.append(data)
+            continue
+        if mn.startswith(("s_", "buffer_", "global_", "flat_", "scratch_", "ds_write", "ds_store")) and \
+                not mn.startswith(("buffer_load", "global_load", "flat_load", "scratch_load")):
+            continue   # writes no VGPR / AGPR
+        first = ops.split(",")[0] if ops else ""
+        dst = set(_regs(first))
+        if dst:
+            live = {k: v for k, v in live.items() if not dst.intersection(k)}
+    return [(d, live.get(d, min_run)) for d in hits]
+
+
+def asm_functions(text):
+    """{name: [(mnemonic, operands)]} from `hipcc -S` output or objdump -d."""
+    if re.search(r"^[0-9a-f]+ <\S+>:$", text, re.M):
+        return {k: [(mn, ops) for _, mn, ops, _ in v] for k, v in functions(text).items()}
+    funcs, cur = {}, None
+    for line in text.splitlines():
+        m = re.match(r"^(_Z\w+):", line)
+        if m:
+            cur = m.group(1)
+            funcs[cur] = []
+            continue
+        if cur is None:
+            continue
+        m = re.match(r"^\s+([a-z_][\w.]*)\s*(.*?)\s*(?:;.*)?$", line)
+        if m and not m.group(1).startswith("."):
+            funcs[cur].append((m.group(1), m.group(2)))
+        if line.strip() == "s_endpgm":
+            cur = None
+    return funcs
+
+
+def scan_repeated_stores(text):
+    """{function: ["<regs> stored N times"]} for every function rule 3 flags."""
+    out = {}
+    for name, insts in asm_functions(text).items():
+        hits = repeated_store_data(insts)
+        if hits:
+            out[name] = [f"{','.join(f'{k}{r}' for k, r in d)} stored {n} times" for d, n in hits]
+    return out
+
+
 def scan(lib=LIB):
     asm = disassemble(lib)
     funcs = functions(asm)
@@ -168,6 +256,7 @@ def scan(lib=LIB):
     packed = [l.strip() for l in asm.splitlines() if PACKED_FP32.search(l)]
     return asm, {"packed_fp32": len(packed), "packed_fp32_examples": packed[:5],
                  "skin_pair_vmcnt": pairs,
+                 "repeated_store_data": scan_repeated_stores(asm),
                  "mfma": {op: len(re.findall(rf"\b{op}\b", asm))
                           for op in sorted(set(re.findall(r"\bv_mfma_\w+", asm)))}}
 
