@@ -58,7 +58,14 @@ extern "C" {
  *         products hi.hi + hi.lo + lo.hi accumulated in fp32 on
  *         v_mfma_f32_16x16x32_f16 (16/3 x the fp32 MFMA rate).  Same error
  *         order as FP32 vs the float64 reference (~1e-7 m); needs |beta| and
- *         the pose features within f16 range and skinning transforms < 1000. */
+ *         the pose features within f16 range and skinning transforms < 1000.
+ *         Known, guarded, not understood: built with packed fp32 VALU
+ *         (v_pk_fma_f32 with an SGPR-pair operand, which the SLP vectorizer
+ *         makes of the LBS unscale), the rest_verts instantiations returned
+ *         wrong x coordinates under memory load; no hardware rule explaining it
+ *         is known.  Correctness rests on the build flag
+ *         -fno-slp-vectorize and on ISA checks that no packed fp32 op exists in
+ *         the library (tests/test_codegen.py, tests/test_gpu_codegen.py). */
 #define MANO_PRECISION_FP32 0
 #define MANO_PRECISION_F16X3 1
 

@@ -30,6 +30,16 @@
 // -- and excluded wait-state hazards, the counted vmcnt barriers, stray
 // stores and spills (tools/debug/h3_root_cause.sh).  Packed
 // fp32 beside MFMA is also the slower form on gfx950 (MI355X_MICROARCH.md).
+//
+// Status, plainly: the miscompute is GUARDED, NOT UNDERSTOOD.  No hardware
+// rule that would explain it is known (the instruction windows of the
+// failing and passing builds differ only in 6-7 vs 1-3 stores in flight,
+// profiles/r03_f16x3_windows.jsonl; no errata are available offline).  This
+// mode is correct because the build flag -fno-slp-vectorize and no_pack()
+// keep the instruction form out, and because tests/test_codegen.py and
+// tests/test_gpu_codegen.py fail on any packed fp32 op in the library.  It
+// stays opt-in (MANO_PRECISION_F16X3); the default fp32 path has no packed
+// fp32 either.
 #include "mano_internal.h"
 #include "mano_span.h"
 
