@@ -135,7 +135,7 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
 
   // ---- one device block, 256-B aligned sub-arrays ----
   struct Part { const void* src; size_t bytes; size_t off; };
-  enum { kBasis, kWeights, kJt, kJs, kParents, kDepth, kPcaB, kPcaM, kZeros, kStatus, kBasis16, kW16, kBasisH3, kNParts };
+  enum { kBasis, kWeights, kJt, kJs, kParents, kDepth, kPcaB, kPcaM, kZeros, kStatus, kBasis16, kW16, kBasisH3, kB16V, kW16V, kNParts };
   std::vector<Part> parts(kNParts);
   parts[kBasis] = {hm.tiles.data(), hm.tiles.size() * 4, 0};
   parts[kWeights] = {hm.weights.data(), hm.weights.size() * 4, 0};
@@ -150,6 +150,8 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   parts[kBasis16] = {hm.b16.data(), hm.b16.size() * 4, 0};
   parts[kW16] = {hm.w16.data(), hm.w16.size() * 4, 0};
   parts[kBasisH3] = {hm.bh3.data(), hm.bh3.size() * 2, 0};
+  parts[kB16V] = {hm.b16v.data(), hm.b16v.size() * 4, 0};
+  parts[kW16V] = {hm.w16v.data(), hm.w16v.size() * 4, 0};
   size_t total = 0;
   for (auto& p : parts) {
     p.off = total;
@@ -159,6 +161,7 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   e = hipMalloc(&block, total);
   if (e != hipSuccess) return hip_fail(e, "hipMalloc(model buffer)");
   for (auto& p : parts) {
+    if (p.bytes == 0) continue;  // no aligned variants for this V
     e = hipMemcpy(static_cast<char*>(block) + p.off, p.src, p.bytes, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
       (void)hipFree(block);
@@ -187,6 +190,8 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   m->dm.status = reinterpret_cast<int32_t*>(at(kStatus));
   m->dm.basis16 = at(kBasis16);
   m->dm.wfrag16 = at(kW16);
+  m->dm.basis16v = hm.b16v.empty() ? nullptr : at(kB16V);
+  m->dm.wfrag16v = hm.w16v.empty() ? nullptr : at(kW16V);
   m->dm.basis_h3 = reinterpret_cast<uint16_t*>(at(kBasisH3));
   m->dm.h3_vposed_unscale = float(std::ldexp(1.0, -hm.basis_exp));
   m->dm.h3_lbs_unscale = float(std::ldexp(1.0, -(kH3FrameExp + kH3WeightExp)));

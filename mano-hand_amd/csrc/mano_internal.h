@@ -25,6 +25,8 @@ struct DeviceModel {
   int32_t* status;      // device status word: MANO_DEVICE_* bits raised by kernels
   float* basis16;       // [n_groups16][3][kTile16Floats]
   float* wfrag16;       // [n_groups16][kWFrag16Floats]
+  float* basis16v;      // [kAlignVariants][n_groups16][3][kTile16Floats] sector-aligned variants,
+  float* wfrag16v;      // [kAlignVariants][n_groups16][kWFrag16Floats]   NULL when V has none (mano_layout.h)
   uint16_t* basis_h3;   // [n_groups16][kH3GroupHalves] f16 bits (f16x3 mode)
   float h3_vposed_unscale;  // 2^-basis_exp: GEMM accumulator -> v_posed
   float h3_lbs_unscale;     // 2^-(kH3FrameExp + kH3WeightExp): LBS sum -> verts

@@ -201,6 +201,23 @@ __device__ __forceinline__ void load_lbs_frags(const float* __restrict__ transfo
   }
 }
 
+// load_lbs_frags for a tile of hands base + (i << lp), i < n_valid (rows past
+// n_valid repeat the last valid hand): blend_skin16's residue-class tiles.
+__device__ __forceinline__ void load_lbs_frags_strided(const float* __restrict__ transforms, int64_t base,
+                                                       int lp, int n_valid, int lane, float (&F)[12][4]) {
+  const int64_t hand = base + (int64_t(min(lane & 15, n_valid - 1)) << lp);
+  const f32x4* A = reinterpret_cast<const f32x4*>(transforms + hand * kTransformFloats) + (lane >> 4) * 3;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const f32x4 v = A[q * 12 + i];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) F[4 * i + e][q] = v[e];
+    }
+  }
+}
+
 // LBS of one 16-hand x 16-vertex tile (mano_np.py:112-115): the 12 transform
 // tiles T_{c,k} = F_{c,k} . W^T (4 MFMAs each, K = 16 joints) applied to the
 // rest vertices p[coord] as out_c = T_c3 + T_c2 z + T_c1 y + T_c0 x (fmaf,
@@ -374,7 +391,7 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
     const float* __restrict__ features, const float* __restrict__ transforms,
     const float* __restrict__ basis16, const float* __restrict__ wfrag16,
     const float* __restrict__ trans, float* __restrict__ verts, float* __restrict__ vposed,
-    int64_t n, int n_verts, int n_groups) {
+    int64_t n, int n_verts, int n_groups, int lp, unsigned shifts, int aligned) {
   // One slot: a basis tile (10 KB) + the group's W fragment (1 KB, with the
   // group's first tile); ring of 3.
   constexpr int kRingF4 = (kGroups16 + 1) * 64;
@@ -402,8 +419,14 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
   __shared__ f32x4 lds[kSlots * kRingF4];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int vstride32 = 3 * n_verts;
-  const int64_t nt16 = (n + 15) / 16;
-  const int64_t n_quads = (nt16 + 3) / 4;
+  // Sector-aligned rows (mano_layout.h, `aligned`): hands are taken in
+  // residue classes r = h mod P (P = 2^lp); quad (r, j) holds hands
+  // 64 P j + P i + r, i = 0..63 (wave w: i = 16 w .. 16 w + 15), whose rows
+  // share one sector phase, so the whole block uses one operand variant
+  // s_r = shifts >> 4 r & 15.  Quads are numbered class-major: the grid's
+  // contiguous eighths (the XCDs, below) each read one or two variants.
+  // Without it (lp = 0): quad j = hands 64 j .. 64 j + 63, the plain layout.
+  const int64_t n_quads = aligned_n_quads(n, lp);
   int64_t u, u_end;
   // Paired ranges: range r goes to block (r % per) * 8 + r / per (per =
   // gridDim / 8), so ranges r and r + 1 sit on one XCD (blocks are dealt to
@@ -441,10 +464,15 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
     const int64_t qs = quad * n_groups;
     const int g0 = int((u > qs ? u : qs) - qs);
     const int g1 = int((u_end < qs + n_groups ? u_end : qs + n_groups) - qs);
-    // A wave past the batch end recomputes the last tile and rewrites its
-    // (identical) values, so every store below is unconditional.
-    const int64_t h0 = min(quad * 4 + wave, nt16 - 1) * 16;
-    const int n_valid = int(n - h0 < 16 ? n - h0 : 16);
+    // This wave's tile: hands h0 + (i << lp), i < n_valid (mano_layout.h).  A
+    // wave past the batch end recomputes the quad's last tile and rewrites
+    // its (identical) values, so every store below is unconditional.
+    const AlignedTile tile = aligned_tile(n, lp, quad, wave);
+    const int64_t h0 = tile.h0;
+    const int n_valid = tile.n_valid;
+    const int shift = aligned ? int((shifts >> (4 * tile.cls)) & 15u) : 0;
+    const float* bvar = basis16 + (aligned ? int64_t(shift) * n_groups * 3 * kTile16Floats : 0);
+    const float* wvar = wfrag16 + (aligned ? int64_t(shift) * n_groups * kWFrag16Floats : 0);
 
     // An opaque lane index per range: keeps hipcc from hoisting lane-dependent
     // addresses out of the range loop, which would hold them in registers --
@@ -458,7 +486,7 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
     float a[kGroups16 * 4];
     float F[12][4];  // LBS A fragments, tile (c, k) = c * 4 + k, resident for the quad
     // A fragments from the X rows: lane's steps 4g..4g+3 are one dwordx4.
-    const int64_t row = min(h0 + (lane & 15), n - 1);
+    const int64_t row = h0 + (int64_t(min(lane & 15, n_valid - 1)) << lp);
     const f32x4* src = reinterpret_cast<const f32x4*>(features + row * kXStride) + (lane >> 4);
 #pragma unroll
     for (int g = 0; g < kGroups16; ++g) {
@@ -466,7 +494,7 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
 #pragma unroll
       for (int q = 0; q < 4; ++q) a[4 * g + q] = v[q];
     }
-    load_lbs_frags(transforms, h0, n, lane, F);
+    load_lbs_frags_strided(transforms, h0, lp, n_valid, lane, F);
     // The lane's 4 rows' translations, held in registers for the range (read
     // from an LDS copy at every group: 0.4952 vs 0.4913 ms with trans, same bits)
     float tv[4][3];
@@ -474,12 +502,13 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int c = 0; c < 3; ++c) tv[r][c] = trans[(h0 + min(row0 + r, n_valid - 1)) * 3 + c];
+        for (int c = 0; c < 3; ++c) tv[r][c] = trans[(h0 + (int64_t(min(row0 + r, n_valid - 1)) << lp)) * 3 + c];
     }
     // ABLATE 4: tiles of 16 rows x n_groups x 64 floats (the aligned scratch layout)
     const int64_t tile_floats = MANO_BS_ABLATE == 4 ? int64_t(n_groups) * 64 : int64_t(vstride32);
     float* vtile = verts + h0 * tile_floats;
     float* ptile = kVposed ? vposed + h0 * tile_floats : nullptr;
+    const int rstride = vstride32 << lp;  // floats between the tile's rows
 
     // The W fragment rides in the slot of the group's first tile (LDS-DMA by
     // wave 2, which has the fewest basis pieces): a global load in the loop
@@ -488,15 +517,15 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
       if (wave == 2) {
         unsigned lane_off = unsigned(lane) * 16u;
         asm volatile("" : "+v"(lane_off));
-        const char* src = reinterpret_cast<const char*>(wfrag16 + int64_t(grp) * kWFrag16Floats);
+        const char* src = reinterpret_cast<const char*>(wvar + int64_t(grp) * kWFrag16Floats);
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + lane_off),
                                          (__attribute__((address_space(3))) void*)(slot + kGroups16 * 64),
                                          16, 0, 0);
       }
     };
-    stage_basis_tile16(basis16, 3 * g0, lds, wave, lane);
+    stage_basis_tile16(bvar, 3 * g0, lds, wave, lane);
     stage_w(g0, lds);
-    stage_basis_tile16(basis16, 3 * g0 + 1, lds + kRingF4, wave, lane);
+    stage_basis_tile16(bvar, 3 * g0 + 1, lds + kRingF4, wave, lane);
     bs_barrier<0>();  // the first two tiles and every prologue load have landed
 #if MANO_BS_STAMP
     {
@@ -517,7 +546,7 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
       f32x4 p[3];
       // Tile 3 grp + q in slot q; tile 3 grp + q + 2 goes to slot (q + 2) % 3.
       prio_up<kDmaPrio>();
-      if constexpr (!(MANO_BS_ABLATE & 16)) stage_basis_tile16(basis16, 3 * grp + 2, lds + 2 * kRingF4, wave, lane);
+      if constexpr (!(MANO_BS_ABLATE & 16)) stage_basis_tile16(bvar, 3 * grp + 2, lds + 2 * kRingF4, wave, lane);
       prio_down<kDmaPrio>();
       const f32x4 wf = lds[kGroups16 * 64 + lane];  // read before slot 0 is re-staged
       if (!kDefer || grp == g0) p[0] = mfma16_tile(a, lds, lane);
@@ -526,7 +555,7 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
       else bs_barrier<kPieces + kStores>();
       if (more) {
         prio_up<kDmaPrio>();
-        if constexpr (!(MANO_BS_ABLATE & 16)) stage_basis_tile16(basis16, 3 * grp + 3, lds, wave, lane);
+        if constexpr (!(MANO_BS_ABLATE & 16)) stage_basis_tile16(bvar, 3 * grp + 3, lds, wave, lane);
         stage_w(grp + 1, lds);
         prio_down<kDmaPrio>();
       }
@@ -535,19 +564,25 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
       else bs_barrier<0>();
       if (more) {
         prio_up<kDmaPrio>();
-        if constexpr (!(MANO_BS_ABLATE & 16)) stage_basis_tile16(basis16, 3 * grp + 4, lds + kRingF4, wave, lane);
+        if constexpr (!(MANO_BS_ABLATE & 16)) stage_basis_tile16(bvar, 3 * grp + 4, lds + kRingF4, wave, lane);
         prio_down<kDmaPrio>();
       }
       p[2] = mfma16_tile(a, lds + 2 * kRingF4, lane);
       if (more) bs_barrier<kPieces>();
       else bs_barrier<0>();
-      int vb = grp * 16;
-      if (vb > n_verts - 16) vb = n_verts - 16;
-      const int voff = 3 * (vb + col);
+      // the lane's vertex in this group (grp, shift uniform: scalar branches)
+      int vx;
+      if (aligned) {
+        vx = aligned_group_vertex(n_verts, shift, grp, col);
+      } else {
+        const int vb = grp * 16 < n_verts - 16 ? grp * 16 : n_verts - 16;
+        vx = vb + col;
+      }
+      const int voff = 3 * vx;
       // byte offset of row hr's point of this lane from the tile base
       auto row_off = [&](int hr) -> unsigned {
-        if constexpr (MANO_BS_ABLATE == 4) return 4u * unsigned((hr * n_groups + grp) * 64 + 3 * col);
-        else return 4u * unsigned(hr * vstride32 + voff);
+        if constexpr (MANO_BS_ABLATE == 4) return 4u * unsigned(((hr << lp) * n_groups + grp) * 64 + 3 * col);
+        else return 4u * unsigned(hr * rstride + voff);
       };
       if constexpr (kVposed) {
         // rest_verts leave before the LBS: their stores drain under its MFMAs
@@ -801,14 +836,33 @@ dim3 persistent_grid(Kernel kernel, const DeviceModel& m, int64_t units, int wor
 
 }  // namespace
 
+// Sector-aligned output rows (mano_layout.h; diagnostic builds: 0 = the
+// round-3 layout, every hand on the plain groups).
+#ifndef MANO_BS_ALIGN
+#define MANO_BS_ALIGN 1
+#endif
 hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features,
                              const float* transforms, const float* trans, float* verts,
                              float* vposed, hipStream_t stream) {
-  const int64_t n_quads = ((n + 15) / 16 + 3) / 4;
+  // The verts rows' sector phases: class r = h mod 2^lp starts at float
+  // a + 3 V r (mod 8), a = the verts address in floats (mod 8); its variant
+  // s_r = (-3 c_r) mod 8 puts the groups on sector boundaries.
+  int lp = 0, aligned = 0;
+  unsigned shifts = 0;
+  const float* b16 = m.basis16;
+  const float* w16 = m.wfrag16;
+  if (MANO_BS_ALIGN && MANO_BS_ABLATE == 0 && m.basis16v && m.wfrag16v) {
+    lp = aligned_period_log2(m.n_verts);
+    shifts = aligned_shifts(m.n_verts, unsigned(reinterpret_cast<uintptr_t>(verts) >> 2) & 7u, lp);
+    b16 = m.basis16v;
+    w16 = m.wfrag16v;
+    aligned = 1;
+  }
+  const int64_t n_quads = aligned_n_quads(n, lp);
   auto launch = [&](auto kernel) {
     hipLaunchKernelGGL(kernel, persistent_grid(kernel, m, n_quads * m.n_groups16, 1, kBlendSkinBlocksPerCU),
-                       dim3(256), 0, stream, features, transforms, m.basis16, m.wfrag16, trans, verts,
-                       vposed, n, m.n_verts, m.n_groups16);
+                       dim3(256), 0, stream, features, transforms, b16, w16, trans, verts,
+                       vposed, n, m.n_verts, m.n_groups16, lp, shifts, aligned);
   };
   if (trans && vposed) launch(blend_skin16_kernel<true, true>);
   else if (trans) launch(blend_skin16_kernel<true, false>);

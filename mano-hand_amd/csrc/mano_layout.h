@@ -59,6 +59,79 @@ constexpr int kGroups16 = (kSteps16 + 3) / 4;  // 10 float4 groups per lane
 constexpr int kTile16Floats = kGroups16 * 64 * 4;   // 2560 floats = 10 KB
 constexpr int kWFrag16Floats = 64 * 4;         // 256 floats per 16-vertex group
 
+// Sector-aligned output rows of blend_skin16 (round 4).  Hand h's verts row
+// starts at float a + 3 V h (a = (verts address / 4) mod 8), so its phase
+// within a 32-B sector, c_h = (a + 3 V h) mod 8, repeats with a period of
+// P = 8 / gcd(3 V, 8) hands (4 for V = 778: rows are 9,336 B apart).  With the
+// 16-vertex groups of hand h shifted by s = (-3 c_h) mod 8 vertices
+// (3 s + c_h = 0 mod 8), every group's 48 floats start and end on a sector
+// boundary, and its 16 point stores write 6 whole sectors (the round-3
+// layout wrote a partial sector at both ends of a group for 3 hands in 4:
+// WRITE_SIZE 1.15x of the verts bytes, 1.23x with rest_verts).  Variant s of
+// the fused kernel's B and W fragments (basis16v / wfrag16v, kAlignVariants
+// of them) maps lane column col of group g to
+//   g <  ga = (V - s) / 16:  vertex s + 16 g + col
+//   g == ga (the edge group): col < s ? col : min(16 ga + col, V - 1)
+// i.e. the edge group holds the row's first s vertices and its last
+// (V - s) mod 16, the row's first and last sectors -- which it shares with
+// the neighbouring hands' rows in any layout.  Duplicate columns (clamped to
+// V - 1) store identical values.  A variant is usable when its edge fits one
+// group and the group count equals n_groups16 (every s for V = 778).
+constexpr int kAlignVariants = 8;
+__host__ __device__ constexpr int aligned_group_vertex(int V, int s, int g, int col) {
+  return g < (V - s) / 16 ? s + 16 * g + col
+         : col < s        ? col
+                          : (16 * ((V - s) / 16) + col < V - 1 ? 16 * ((V - s) / 16) + col : V - 1);
+}
+constexpr bool aligned_variant_ok(int V, int s, int n_groups16) {
+  return V >= s + 16 && s + (V - s) % 16 <= 16 &&
+         (V - s) / 16 + ((V - s) % 16 != 0 || s > 0 ? 1 : 0) == n_groups16;
+}
+// log2 of the period P (hands) of the sector phase of rows of V vertices.
+constexpr int aligned_period_log2(int V) {
+  return (3 * V) % 8 == 0 ? 0 : (3 * V * 2) % 8 == 0 ? 1 : (3 * V * 4) % 8 == 0 ? 2 : 3;
+}
+// Variant of class r's hands for a verts row base at float phase a (mod 8):
+// s_r = (-3 c_r) mod 8 with c_r = (a + 3 V r) mod 8, four bits per class.
+constexpr unsigned aligned_shifts(int V, unsigned a, int lp) {
+  unsigned code = 0;
+  for (int r = 0; r < (1 << lp); ++r) {
+    const unsigned c = (a + 3u * unsigned(V) * unsigned(r)) & 7u;
+    code |= ((8u - (3u * c) % 8u) % 8u) << (4 * r);
+  }
+  return code;
+}
+// blend_skin16's hand tiles in residue classes (P = 2^lp; lp = 0 is the plain
+// layout): quad (r, j) holds hands 64 P j + P i + r, i = 0..63, wave w of the
+// block the 16 with i = 16 w .. 16 w + 15.  Quads are numbered class-major.
+__host__ __device__ inline int64_t aligned_class_quads(int64_t n, int lp, int r) {
+  return n > r ? ((n - 1 - r) >> (6 + lp)) + 1 : 0;
+}
+__host__ __device__ inline int64_t aligned_n_quads(int64_t n, int lp) {
+  int64_t q = 0;
+  for (int r = 0; r < (1 << lp); ++r) q += aligned_class_quads(n, lp, r);
+  return q;
+}
+// Wave `wave`'s tile of quad `quad`: its first hand h0 (hands h0 + (i << lp),
+// i < n_valid, are in the batch) and the quad's class.  A wave whose tile is
+// past the batch end takes the quad's last tile (it recomputes and rewrites
+// identical values).
+struct AlignedTile {
+  int64_t h0;
+  int n_valid;
+  int cls;
+};
+__host__ __device__ inline AlignedTile aligned_tile(int64_t n, int lp, int64_t quad, int wave) {
+  int cls = 0;
+  int64_t j = quad;
+  while (cls + 1 < (1 << lp) && j >= aligned_class_quads(n, lp, cls)) j -= aligned_class_quads(n, lp, cls++);
+  const int64_t qbase = (j << (6 + lp)) + cls;
+  int64_t h0 = qbase + (int64_t(16 * wave) << lp);
+  if (h0 >= n) h0 = qbase + (int64_t(16 * int(((n - 1 - qbase) >> lp) >> 4)) << lp);
+  const int64_t left = ((n - 1 - h0) >> lp) + 1;
+  return AlignedTile{h0, int(left < 16 ? left : 16), cls};
+}
+
 // f16x3 precision mode (mano_kernels_h3.hip): every fp32 operand x is carried
 // as an unevaluated pair of halves x = hi + lo (hi = f16(x), lo = f16(x - hi),
 // 22 significant bits) and each product as hi.hi + hi.lo + lo.hi on
@@ -91,6 +164,9 @@ struct HostModel {
   std::vector<float> tiles;     // blend_kernel B fragments [n_col_tiles][kKGroups][64][4]
   std::vector<float> b16;       // blend_skin16 B fragments [n_groups16][3][kTile16Floats]
   std::vector<float> w16;       // LBS weight fragments [n_groups16][kWFrag16Floats]
+  std::vector<float> b16v;      // sector-aligned variants [kAlignVariants][n_groups16][3][kTile16Floats]
+  std::vector<float> w16v;      //   and their W fragments [kAlignVariants][n_groups16][kWFrag16Floats]
+                                //   (empty when some variant does not fit V)
   std::vector<uint16_t> bh3;    // f16x3 pieces [n_groups16][kH3GroupHalves]
   std::vector<float> weights;   // [V][16]
   std::vector<float> jt, js;    // J_regressor . template [16][3], . shapedirs [16][3][10]

@@ -123,32 +123,45 @@ bool pack_model(int n_verts, const double* mesh_template, const double* mesh_sha
           }
           tiles[((size_t(t) * kKGroups + g) * 64 + l) * 4 + q] = v;
         }
-  // 16x16x4 fused layout: group g = 16 vertices from min(16g, V-16).
+  // 16x16x4 fused layout: group g = 16 vertices from min(16g, V-16); and
+  // the sector-aligned variants (mano_layout.h aligned_group_vertex).
   const int n_groups16 = (V + 15) / 16;
+  auto fill16 = [&](auto vertex_of, float* b16, float* w16) {
+    for (int g = 0; g < n_groups16; ++g) {
+      for (int l = 0; l < 64; ++l) {
+        const int v = vertex_of(g, l & 15);
+        for (int st = 0; st < 4; ++st)
+          if (v < V)
+            w16[size_t(g) * kWFrag16Floats + l * 4 + st] =
+                float(skinning_weights[size_t(v) * kJoints + 4 * st + (l >> 4)]);
+        for (int q = 0; q < 3; ++q)
+          for (int gg = 0; gg < kGroups16; ++gg)
+            for (int qq = 0; qq < 4; ++qq) {
+              const int k = 4 * (4 * gg + qq) + (l >> 4);
+              float val = 0.f;
+              if (k <= kK && v < V) {
+                const size_t colv = size_t(v) * 3 + q;
+                val = k < kShape ? float(mesh_shape_basis[colv * kShape + k])
+                      : k < kK   ? float(mesh_pose_basis[colv * kPoseFeats + (k - kShape)])
+                                 : float(mesh_template[colv]);
+              }
+              b16[((size_t(g) * 3 + q) * kGroups16 + gg) * 256 + l * 4 + qq] = val;
+            }
+      }
+    }
+  };
   std::vector<float> b16(size_t(n_groups16) * 3 * kTile16Floats, 0.f);
   std::vector<float> w16(size_t(n_groups16) * kWFrag16Floats, 0.f);
-  for (int g = 0; g < n_groups16; ++g) {
-    const int vb = std::max(0, std::min(16 * g, V - 16));
-    for (int l = 0; l < 64; ++l) {
-      const int v = vb + (l & 15);
-      for (int st = 0; st < 4; ++st)
-        if (v < V)
-          w16[size_t(g) * kWFrag16Floats + l * 4 + st] =
-              float(skinning_weights[size_t(v) * kJoints + 4 * st + (l >> 4)]);
-      for (int q = 0; q < 3; ++q)
-        for (int gg = 0; gg < kGroups16; ++gg)
-          for (int qq = 0; qq < 4; ++qq) {
-            const int k = 4 * (4 * gg + qq) + (l >> 4);
-            float val = 0.f;
-            if (k <= kK && v < V) {
-              const size_t colv = size_t(v) * 3 + q;
-              val = k < kShape ? float(mesh_shape_basis[colv * kShape + k])
-                    : k < kK   ? float(mesh_pose_basis[colv * kPoseFeats + (k - kShape)])
-                               : float(mesh_template[colv]);
-            }
-            b16[((size_t(g) * 3 + q) * kGroups16 + gg) * 256 + l * 4 + qq] = val;
-          }
-    }
+  fill16([&](int g, int col) { return std::max(0, std::min(16 * g, V - 16)) + col; }, b16.data(), w16.data());
+  bool variants_ok = true;
+  for (int sh = 0; sh < kAlignVariants; ++sh) variants_ok = variants_ok && aligned_variant_ok(V, sh, n_groups16);
+  std::vector<float> b16v, w16v;
+  if (variants_ok) {
+    b16v.assign(size_t(kAlignVariants) * b16.size(), 0.f);
+    w16v.assign(size_t(kAlignVariants) * w16.size(), 0.f);
+    for (int sh = 0; sh < kAlignVariants; ++sh)
+      fill16([&](int g, int col) { return aligned_group_vertex(V, sh, g, col); }, b16v.data() + sh * b16.size(),
+             w16v.data() + sh * w16.size());
   }
   // f16x3 pieces (mano_internal.h): basis x 2^basis_exp with the largest
   // entry at most 2^14, split hi/lo; weights x 2^kH3WeightExp.
@@ -200,6 +213,8 @@ bool pack_model(int n_verts, const double* mesh_template, const double* mesh_sha
   out.tiles = std::move(tiles);
   out.b16 = std::move(b16);
   out.w16 = std::move(w16);
+  out.b16v = std::move(b16v);
+  out.w16v = std::move(w16v);
   out.bh3 = std::move(bh3);
   out.weights = std::move(wts);
   out.jt = std::move(jt);

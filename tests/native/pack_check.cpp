@@ -100,6 +100,74 @@ void check_mesh(int V, uint64_t seed) {
           }
     }
   }
+  // sector-aligned variants (mano_layout.h): present iff every shift fits V;
+  // variant s group g lane col holds aligned_group_vertex's vertex; the
+  // groups of a variant cover every vertex; for a row at float phase c the
+  // groups g < ga of variant (-3 c) mod 8 start on a sector boundary.
+  bool all_ok = true;
+  for (int sh = 0; sh < kAlignVariants; ++sh) all_ok = all_ok && aligned_variant_ok(V, sh, n_groups);
+  EXPECT(all_ok == !hm.b16v.empty() && hm.b16v.size() == hm.w16v.size() * 3 * kTile16Floats / kWFrag16Floats,
+         "V=%d variants present %d, sizes %zu %zu", V, int(all_ok), hm.b16v.size(), hm.w16v.size());
+  if (V == 778) EXPECT(all_ok, "V=778 must have every aligned variant");
+  for (int sh = 0; sh < kAlignVariants && !hm.b16v.empty(); ++sh) {
+    const int ga = (V - sh) / 16;
+    std::vector<int> seen(V, 0);
+    for (int g = 0; g < n_groups; ++g)
+      for (int l = 0; l < 64; ++l) {
+        const int v = aligned_group_vertex(V, sh, g, l & 15);
+        EXPECT(v >= 0 && v < V, "V=%d s %d g %d col %d vertex %d", V, sh, g, l & 15, v);
+        if (v < 0 || v >= V) continue;
+        seen[v] = 1;
+        if (g < ga) EXPECT(v == sh + 16 * g + (l & 15), "V=%d s %d aligned group %d", V, sh, g);
+        for (int st = 0; st < 4; ++st)
+          EXPECT(hm.w16v[(size_t(sh) * n_groups + g) * 256 + l * 4 + st] ==
+                     float(w[size_t(v) * kJoints + 4 * st + (l >> 4)]), "V=%d w16v s %d g %d l %d", V, sh, g, l);
+        for (int c = 0; c < 3; ++c)
+          for (int gg = 0; gg < kGroups16; ++gg)
+            for (int qq = 0; qq < 4; ++qq) {
+              const int k = 4 * (4 * gg + qq) + (l >> 4);
+              const float want = k <= kK ? float(basis(k, 3 * v + c)) : 0.f;
+              EXPECT(hm.b16v[(((size_t(sh) * n_groups + g) * 3 + c) * kGroups16 + gg) * 256 + l * 4 + qq] == want,
+                     "V=%d b16v s %d g %d c %d k %d", V, sh, g, c, k);
+            }
+      }
+    for (int v = 0; v < V; ++v) EXPECT(seen[v], "V=%d s %d vertex %d not covered", V, sh, v);
+  }
+  for (unsigned phase = 0; phase < 8; ++phase) {
+    const int sh = int(aligned_shifts(V, phase, 0) & 15u);
+    for (int g = 0; g < (V - sh) / 16; ++g)
+      EXPECT((phase + 3 * unsigned(aligned_group_vertex(V, sh, g, 0))) % 8 == 0, "V=%d phase %u group %d", V, phase, g);
+  }
+  // blend_skin16's residue-class hand tiles: over every quad and wave, the
+  // rows cover each hand of the batch, only hands of the batch, and a
+  // quad's rows all share one class; rows of class r sit at the phase its
+  // shift aligns.
+  const int lp = aligned_period_log2(V);
+  for (int64_t n : {1, 2, 3, 5, 63, 64, 65, 255, 256, 257, 511, 1000, 1027, 4097}) {
+    std::vector<int> hit(size_t(n), 0);
+    const int64_t nq = aligned_n_quads(n, lp);
+    for (int64_t q = 0; q < nq; ++q)
+      for (int wv = 0; wv < 4; ++wv) {
+        const AlignedTile t = aligned_tile(n, lp, q, wv);
+        EXPECT(t.n_valid >= 1 && t.n_valid <= 16 && t.h0 >= 0 && t.h0 < n, "V=%d n %lld q %lld w %d", V,
+               (long long)n, (long long)q, wv);
+        for (int i = 0; i < 16; ++i) {
+          const int64_t h = t.h0 + (int64_t(i < t.n_valid ? i : t.n_valid - 1) << lp);
+          EXPECT(h >= 0 && h < n && (h & ((1 << lp) - 1)) == t.cls, "V=%d n %lld hand %lld", V, (long long)n,
+                 (long long)h);
+          if (h >= 0 && h < n) hit[size_t(h)] = 1;
+        }
+      }
+    for (int64_t h = 0; h < n; ++h) EXPECT(hit[size_t(h)], "V=%d n %lld hand %lld not covered", V, (long long)n, (long long)h);
+    for (unsigned a = 0; a < 8; ++a) {
+      const unsigned code = aligned_shifts(V, a, lp);
+      for (int64_t h = 0; h < 64 && h < n; ++h) {
+        const int sh = int((code >> (4 * (h & ((1 << lp) - 1)))) & 15u);
+        EXPECT((a + 3u * unsigned(V) * unsigned(h) + 3u * unsigned(sh)) % 8 == 0, "V=%d a %u hand %lld", V, a,
+               (long long)h);
+      }
+    }
+  }
   // f16x3 pieces: hi + lo of the basis x 2^basis_exp and of the weights x 2^kH3WeightExp
   const double bscale = std::ldexp(1.0, hm.basis_exp), wscale = std::ldexp(1.0, kH3WeightExp);
   EXPECT(hm.bh3.size() == size_t(n_groups) * kH3GroupHalves, "bh3 size");

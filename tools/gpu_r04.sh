@@ -20,9 +20,9 @@ step() {  # name timeout cmd...
 for s in ${STEPS:-tests align pmc bench c4}; do
   case $s in
     tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 180 --timeout-method thread ${PYTEST_ARGS:-} ;;
-    align) step align_bound 400 python tools/debug/align_bound.py libmano_hip.so libmano_hip_abl4.so --reps 3 ;;
+    align) step align_bound 500 python tools/debug/align_bound.py ${ALIGN_LIBS:-libmano_hip.so libmano_hip_abl4.so} --reps 3 ;;
     pmc)
-      for lib in libmano_hip.so libmano_hip_abl4.so; do
+      for lib in ${PMC_LIBS:-libmano_hip.so libmano_hip_abl4.so}; do
         for what in verts rest; do
           for c in WRITE_SIZE FETCH_SIZE; do
             step pmc_${lib%.so}_${what}_$c 90 rocprofv3 --pmc $c -d $OUT/pmc_${lib%.so}_${what}_$c -o p --output-format csv -- python tools/debug/align_bound.py --loop $lib $what 20
