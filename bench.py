@@ -498,6 +498,10 @@ def main(argv=None):
             # (mano_gather), or every GPU's (mano_allgather)
             gv = torch.empty((B * world, V, 3), device=dev)
             gj = torch.empty((B * world, 16, 3), device=dev)
+            # this rank's shard is computed in place, in its rows of the
+            # assembled buffers: the gather moves only the peers' shards
+            verts = gv[rank * B:(rank + 1) * B]
+            joints = gj[rank * B:(rank + 1) * B]
 
     def do_gather(which):
         if gatherer is not None:
@@ -612,7 +616,9 @@ def main(argv=None):
                                 "allgather": "mano_allgather: RCCL ring ncclAllGather"}[impl]
                                if gatherer is not None else "gloo rehearsal through the host")
         gather_info["timing"] = ("HIP events on rank 0's launch stream around the gather (verts + "
-                                 "joints) of every sampled timed step, after that step's kernels")
+                                 "joints) of every sampled timed step, after that step's kernels; "
+                                 "each rank's own shard is computed in place in its rows of the "
+                                 "assembled buffers, so only the peers' shards move")
 
     def span(a, b, evs):
         return float(np.mean([e[a].elapsed_time(e[b]) for e in evs]))
@@ -685,7 +691,8 @@ def main(argv=None):
         cmp_info = gather_stats(other_impl, world, B, float(np.mean(cms)))
         cmp_info.update({"ms_min": float(np.min(cms)), "ms_max": float(np.max(cms)), "reps": len(cms),
                          "timing": "after the timed region, the gather alone back to back (no forward "
-                                   "in between), HIP events on rank 0's stream"})
+                                   "in between), HIP events on rank 0's stream; out of place (each rank's "
+                                   "own shard is copied too, unlike the timed form's in-place shard)"})
         if rank == 0:
             chk = check_gather(model, wl["seed"], B, world, gv, gj, with_trans)
             cmp_info["bit_exact"] = chk["bit_exact"]

@@ -237,7 +237,9 @@ int mano_synthetic_inputs(int device, uint64_t seed, int64_t first_index, int64_
  * lands rank r's bytes at recv + sum(rank_bytes[0..r-1]) (rank_bytes: the
  * per-rank sizes, read on root only; NULL = every rank sends send_bytes), so
  * ragged contiguous shards need no padding.  recv is read on root only.
- * Asynchronous on `stream`.  RCCL (librccl.so.1) is loaded on first use. */
+ * The root may produce its own shard in place (send == recv + its offset):
+ * then nothing is copied for it.  Asynchronous on `stream`.  RCCL
+ * (librccl.so.1) is loaded on first use. */
 #define MANO_COMM_ID_BYTES 128
 typedef struct mano_comm mano_comm;
 int mano_comm_unique_id(unsigned char* id /* [MANO_COMM_ID_BYTES] */);
@@ -248,7 +250,8 @@ int mano_gather(mano_comm* comm, const void* send, size_t send_bytes, void* recv
                 const size_t* rank_bytes, int32_t root, void* stream);
 /* Every rank receives every shard: RCCL's ring ncclAllGather of equal
  * `send_bytes` shards, rank r's bytes at recv + r * send_bytes on EVERY rank
- * (recv holds n_ranks * send_bytes).  The comparison form for mano_gather
+ * (recv holds n_ranks * send_bytes; in place when send == recv + rank *
+ * send_bytes, as RCCL allows).  The comparison form for mano_gather
  * (a ring is bound by one link per hop), and the call for
  * callers that want the whole batch on every device.  Asynchronous on
  * `stream`. */

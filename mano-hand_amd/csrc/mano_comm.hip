@@ -200,7 +200,9 @@ int mano_gather(mano_comm* c, const void* send, size_t send_bytes, void* recv,
   if (guard.err != hipSuccess)
     return fail(MANO_EHIP, "hipSetDevice: %s", hipGetErrorString(guard.err));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (is_root && send_bytes > 0) {
+  // The root's own shard: copied into place, unless the caller computed it
+  // there (send == its slot of recv: nothing to move).
+  if (is_root && send_bytes > 0 && send != static_cast<const char*>(recv) + off[root]) {
     hipError_t e = hipMemcpyAsync(static_cast<char*>(recv) + off[root], send, send_bytes,
                                   hipMemcpyDeviceToDevice, s);
     if (e != hipSuccess) return fail(MANO_EHIP, "hipMemcpyAsync: %s", hipGetErrorString(e));

@@ -157,7 +157,8 @@ def test_bench_one_rank_nccl_process_group(impl):
     assert line["gather_check"]["bit_exact"], line["gather_check"]
     assert line["correctness"]["pass"] and line["correctness"]["ranks_checked"] == 1, line["correctness"]
     g = line["gather"]
-    assert g["impl"] == impl and g["ms"] > 0 and g["bytes_to_gpu0"] == 0
+    # one rank: its shard is computed in place, the timed gather moves nothing
+    assert g["impl"] == impl and g["ms"] >= 0 and g["bytes_to_gpu0"] == 0
     c = g["compare"]
     assert c["impl"] == ("allgather" if impl == "sendrecv" else "sendrecv")
     assert c["ms"] > 0 and c["reps"] >= 1 and c["bit_exact"]
