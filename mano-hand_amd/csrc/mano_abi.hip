@@ -135,7 +135,7 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
 
   // ---- one device block, 256-B aligned sub-arrays ----
   struct Part { const void* src; size_t bytes; size_t off; };
-  enum { kBasis, kWeights, kJt, kJs, kParents, kDepth, kPcaB, kPcaM, kZeros, kStatus, kBasis16, kW16, kBasisH3, kB16V, kW16V, kNParts };
+  enum { kBasis, kWeights, kJt, kJs, kParents, kDepth, kPcaB, kPcaM, kZeros, kStatus, kBasis16, kW16, kBasisH3, kB16V, kW16V, kTilesV, kNParts };
   std::vector<Part> parts(kNParts);
   parts[kBasis] = {hm.tiles.data(), hm.tiles.size() * 4, 0};
   parts[kWeights] = {hm.weights.data(), hm.weights.size() * 4, 0};
@@ -152,6 +152,7 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   parts[kBasisH3] = {hm.bh3.data(), hm.bh3.size() * 2, 0};
   parts[kB16V] = {hm.b16v.data(), hm.b16v.size() * 4, 0};
   parts[kW16V] = {hm.w16v.data(), hm.w16v.size() * 4, 0};
+  parts[kTilesV] = {hm.tiles_v.data(), hm.tiles_v.size() * 4, 0};
   size_t total = 0;
   for (auto& p : parts) {
     p.off = total;
@@ -179,6 +180,7 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   m->block = block;
   auto at = [&](int i) { return reinterpret_cast<float*>(b + parts[i].off); };
   m->dm.basis_tiles = at(kBasis);
+  m->dm.basis_tiles_v = hm.tiles_v.empty() ? nullptr : at(kTilesV);
   m->dm.weights = at(kWeights);
   m->dm.joint_template = at(kJt);
   m->dm.joint_shape = at(kJs);

@@ -14,6 +14,7 @@ namespace mano {
 // Device-resident model buffer (float32, layouts chosen for the kernels).
 struct DeviceModel {
   float* basis_tiles;   // [n_col_tiles][kKGroups][64][4] MFMA B fragments
+  float* basis_tiles_v; // [kAlignVariants][n_col_tiles][...] sector-aligned variants (NULL: none, mano_layout.h)
   float* weights;       // [V][16] skinning weights
   float* joint_template;// [16][3]   J_regressor . mesh_template       (float64 fold)
   float* joint_shape;   // [16][3][10] J_regressor . mesh_shape_basis (float64 fold)

@@ -21,6 +21,12 @@
 #include "mano_internal.h"
 #include "mano_span.h"
 
+// Sector-aligned output rows of blend_skin16 and the unfused blend (mano_layout.h;
+// diagnostic builds: 0 = the round-3 layouts, every hand on the plain tiles).
+#ifndef MANO_BS_ALIGN
+#define MANO_BS_ALIGN 1
+#endif
+
 namespace mano {
 namespace {
 
@@ -67,20 +73,23 @@ __device__ __forceinline__ f32x16 mfma_tile(const float (&a)[kKGroups * 4], cons
 // 0.3629-0.3669 vs 0.3676-0.3765 ms with plain global stores, the LBS after it
 // 0.288 vs 0.290 (same box, same bits); sc1 took the blend to 0.395
 // (profiles/r03q_ab_blend_store_policy.jsonl); nontemporal stores to 0.60
-// (partial lines: rows are 9,336 B apart).  Rows past the batch end fall
-// outside the tile's buffer and are dropped.
+// (partial lines: rows are 9,336 B apart).  The tile's rows are hands
+// h0 + (hr << lp), hr < n_valid (residue-class tiles, mano_layout.h); rows
+// past n_valid and columns past the row end fall outside the buffer and are
+// dropped.
 __device__ __forceinline__ void store_vposed_tile(float* __restrict__ vposed, const f32x16& acc,
-                                                  int64_t h0, int col, int64_t n, int n_cols,
+                                                  int64_t h0, int lp, int n_valid, int col, int n_cols,
                                                   int hi) {
   // D[hand][col]: col = lane & 31, hand = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
-  const int64_t valid = n - h0 < 32 ? n - h0 : 32;
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc(vposed + h0 * n_cols, 0, int(valid * n_cols * 4), 0x00020000);
+  const int rstride = n_cols << lp;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(vposed + h0 * n_cols, 0, ((n_valid - 1) * rstride + n_cols) * 4,
+                                                    0x00020000);
   if (col < n_cols) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int hr = (r & 3) + 8 * (r >> 2) + 4 * hi;
       const float x = acc[r];  // a scalar first: __builtin_bit_cast of a vector element reads element 0
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), rs, 4 * (hr * n_cols + col), 0, 1 /* sc0 */);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), rs, 4 * (hr * rstride + col), 0, 1 /* sc0 */);
     }
   }
 }
@@ -101,44 +110,49 @@ __device__ __forceinline__ void stage_basis_tile16(const float* __restrict__ bas
   }
 }
 
+// One block per quad of 4 32-hand tiles (residue classes, mano_layout.h,
+// lq = 7): with `aligned` the tiles' rows share one sector phase and the
+// block uses column-tile variant sigma_r (shifts >> 4 r & 15), so every
+// 32-float row segment a tile stores starts on a sector boundary.
 __global__ __launch_bounds__(256, 2) void blend_kernel(
     const float* __restrict__ features, const float* __restrict__ basis_tiles,
-    float* __restrict__ vposed, int64_t n, int n_cols, int n_col_tiles) {
+    float* __restrict__ vposed, int64_t n, int n_cols, int n_col_tiles, int lp, unsigned shifts, int aligned) {
   __shared__ f32x4 bs[2][kKGroups * 64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t ht = int64_t(blockIdx.x) * 4 + wave;
-  const int64_t n_ht = (n + kHandTile - 1) / kHandTile;
-  const bool active = ht < n_ht;
+  // A wave past the batch end recomputes the quad's last tile (identical values).
+  const AlignedTile tile = aligned_tile(n, lp, blockIdx.x, wave, 7);
+  const int sigma = aligned ? int((shifts >> (4 * tile.cls)) & 15u) : 0;
+  const float* tiles = basis_tiles + (aligned ? int64_t(sigma) * n_col_tiles * kTileFloats : 0);
 
   // A fragments of v_mfma_f32_32x32x2_f32: step s holds X[hand = lane & 31][k =
-  // 2 s + (lane >> 5)] (X rows past the batch end repeat the last hand).
+  // 2 s + (lane >> 5)] (rows past the tile's valid hands repeat its last one).
   float a[kKGroups * 4];
   {
-    const int64_t row = min((active ? ht : 0) * kHandTile + (lane & 31), n - 1);
+    const int64_t row = tile.h0 + (int64_t(min(lane & 31, tile.n_valid - 1)) << lp);
     const float* x = features + row * kXStride;
 #pragma unroll
     for (int s = 0; s < kKGroups * 4; ++s) a[s] = s < kKSteps ? x[x_pos(2 * s + (lane >> 5))] : 0.f;
   }
 
-  stage_basis_tile(basis_tiles, 0, bs[0], wave, lane);
+  stage_basis_tile(tiles, 0, bs[0], wave, lane);
   __syncthreads();
 
   const int hi = lane >> 5;
   const int col_in_tile = lane & 31;
-  const int64_t h0 = ht * kHandTile;
+  auto col_of = [&](int t) { return aligned ? aligned_tile_col(n_cols, sigma, t, col_in_tile) : t * kColTile + col_in_tile; };
   // The template is row k = 145 of the basis (X[:, 145] = 1), so the MFMA chain
   // yields v_posed directly.  Tile t's stores are issued one iteration late,
   // before tile t+2's LDS-DMA, so the barrier's vmcnt(0) only waits on old
   // stores and the DMA the MFMA chain has already hidden.
   f32x16 prev = {};
   for (int t = 0; t < n_col_tiles; ++t) {
-    if (active && t > 0) store_vposed_tile(vposed, prev, h0, (t - 1) * kColTile + col_in_tile, n, n_cols, hi);
-    if (t + 1 < n_col_tiles) stage_basis_tile(basis_tiles, t + 1, bs[(t + 1) & 1], wave, lane);
+    if (t > 0) store_vposed_tile(vposed, prev, tile.h0, lp, tile.n_valid, col_of(t - 1), n_cols, hi);
+    if (t + 1 < n_col_tiles) stage_basis_tile(tiles, t + 1, bs[(t + 1) & 1], wave, lane);
     prev = mfma_tile(a, bs[t & 1], lane);
     __syncthreads();
   }
-  if (active) store_vposed_tile(vposed, prev, h0, (n_col_tiles - 1) * kColTile + col_in_tile, n, n_cols, hi);
+  store_vposed_tile(vposed, prev, tile.h0, lp, tile.n_valid, col_of(n_col_tiles - 1), n_cols, hi);
 }
 
 // ---------------------------------------------------------------------------
@@ -790,10 +804,21 @@ hipError_t launch_synthetic_inputs(uint64_t seed, int64_t first, int64_t n, floa
 
 hipError_t launch_blend(const DeviceModel& m, int64_t n, const float* features, float* vposed,
                         hipStream_t stream) {
-  const int64_t n_ht = (n + kHandTile - 1) / kHandTile;
-  const int64_t blocks = (n_ht + 3) / 4;
+  // v_posed rows' sector phases (mano_layout.h): class r of the rows starts at
+  // float a + 3 V r (mod 8); its column tiles are shifted onto sector
+  // boundaries (MANO_BS_ALIGN 0: the plain tiles).
+  int lp = 0, aligned = 0;
+  unsigned shifts = 0;
+  const float* tiles = m.basis_tiles;
+  if (MANO_BS_ALIGN && m.basis_tiles_v) {
+    lp = aligned_period_log2(m.n_verts);
+    shifts = aligned_col_shifts(m.n_verts, unsigned(reinterpret_cast<uintptr_t>(vposed) >> 2) & 7u, lp);
+    tiles = m.basis_tiles_v;
+    aligned = 1;
+  }
+  const int64_t blocks = aligned_n_quads(n, lp, 7);
   hipLaunchKernelGGL(blend_kernel, dim3(unsigned(blocks)), dim3(256), 0, stream, features,
-                     m.basis_tiles, vposed, n, m.n_cols, m.n_col_tiles);
+                     tiles, vposed, n, m.n_cols, m.n_col_tiles, lp, shifts, aligned);
   return hipGetLastError();
 }
 
@@ -836,11 +861,6 @@ dim3 persistent_grid(Kernel kernel, const DeviceModel& m, int64_t units, int wor
 
 }  // namespace
 
-// Sector-aligned output rows (mano_layout.h; diagnostic builds: 0 = the
-// round-3 layout, every hand on the plain groups).
-#ifndef MANO_BS_ALIGN
-#define MANO_BS_ALIGN 1
-#endif
 hipError_t launch_blend_skin(const DeviceModel& m, int64_t n, const float* features,
                              const float* transforms, const float* trans, float* verts,
                              float* vposed, hipStream_t stream) {

@@ -101,15 +101,17 @@ constexpr unsigned aligned_shifts(int V, unsigned a, int lp) {
   }
   return code;
 }
-// blend_skin16's hand tiles in residue classes (P = 2^lp; lp = 0 is the plain
-// layout): quad (r, j) holds hands 64 P j + P i + r, i = 0..63, wave w of the
-// block the 16 with i = 16 w .. 16 w + 15.  Quads are numbered class-major.
-__host__ __device__ inline int64_t aligned_class_quads(int64_t n, int lp, int r) {
-  return n > r ? ((n - 1 - r) >> (6 + lp)) + 1 : 0;
+// The hand tiles of the kernels that use the variants, in residue classes
+// (P = 2^lp; lp = 0 is the plain layout): a block's quad (r, j) holds the
+// 2^lq hands 2^lq P j + P i + r, i < 2^lq, wave w of the block the tile of
+// T = 2^(lq - 2) hands with i = T w .. T w + T - 1 (blend_skin16: lq = 6, 16-hand
+// tiles; blend: lq = 7, 32-hand tiles).  Quads are numbered class-major.
+__host__ __device__ inline int64_t aligned_class_quads(int64_t n, int lp, int r, int lq = 6) {
+  return n > r ? ((n - 1 - r) >> (lq + lp)) + 1 : 0;
 }
-__host__ __device__ inline int64_t aligned_n_quads(int64_t n, int lp) {
+__host__ __device__ inline int64_t aligned_n_quads(int64_t n, int lp, int lq = 6) {
   int64_t q = 0;
-  for (int r = 0; r < (1 << lp); ++r) q += aligned_class_quads(n, lp, r);
+  for (int r = 0; r < (1 << lp); ++r) q += aligned_class_quads(n, lp, r, lq);
   return q;
 }
 // Wave `wave`'s tile of quad `quad`: its first hand h0 (hands h0 + (i << lp),
@@ -121,15 +123,38 @@ struct AlignedTile {
   int n_valid;
   int cls;
 };
-__host__ __device__ inline AlignedTile aligned_tile(int64_t n, int lp, int64_t quad, int wave) {
+__host__ __device__ inline AlignedTile aligned_tile(int64_t n, int lp, int64_t quad, int wave, int lq = 6) {
+  const int lt = lq - 2;  // log2 of the tile's hands
   int cls = 0;
   int64_t j = quad;
-  while (cls + 1 < (1 << lp) && j >= aligned_class_quads(n, lp, cls)) j -= aligned_class_quads(n, lp, cls++);
-  const int64_t qbase = (j << (6 + lp)) + cls;
-  int64_t h0 = qbase + (int64_t(16 * wave) << lp);
-  if (h0 >= n) h0 = qbase + (int64_t(16 * int(((n - 1 - qbase) >> lp) >> 4)) << lp);
+  while (cls + 1 < (1 << lp) && j >= aligned_class_quads(n, lp, cls, lq))
+    j -= aligned_class_quads(n, lp, cls++, lq);
+  const int64_t qbase = (j << (lq + lp)) + cls;
+  int64_t h0 = qbase + (int64_t(wave << lt) << lp);
+  if (h0 >= n) h0 = qbase + (int64_t((int(((n - 1 - qbase) >> lp) >> lt)) << lt) << lp);
   const int64_t left = ((n - 1 - h0) >> lp) + 1;
-  return AlignedTile{h0, int(left < 16 ? left : 16), cls};
+  return AlignedTile{h0, int(left < (1 << lt) ? left : (1 << lt)), cls};
+}
+// The unfused blend GEMM's column tiles (v_mfma_f32_32x32x2_f32, 32 floats of
+// a v_posed row each) on sector boundaries: for a row at float phase c the
+// tiles are shifted by sigma = (8 - c) mod 8 floats; variant sigma's tile t
+// column j is
+//   t <  ta = (C - sigma) / 32:  sigma + 32 t + j
+//   t == ta (the edge tile):     j < sigma ? j : 32 ta + j   (>= C: not stored)
+// (C = 3 V columns).  Usable when the edge fits one tile and the tile count
+// equals n_col_tiles (every sigma for V = 778: 73 tiles).
+__host__ __device__ constexpr int aligned_tile_col(int C, int sigma, int t, int j) {
+  return t < (C - sigma) / 32 ? sigma + 32 * t + j : j < sigma ? j : 32 * ((C - sigma) / 32) + j;
+}
+constexpr bool aligned_col_variant_ok(int C, int sigma, int n_col_tiles) {
+  return C >= sigma + 32 && sigma + (C - sigma) % 32 <= 32 &&
+         (C - sigma) / 32 + ((C - sigma) % 32 != 0 || sigma > 0 ? 1 : 0) == n_col_tiles;
+}
+// Column shift of class r's rows for a row base at float phase a (mod 8).
+constexpr unsigned aligned_col_shifts(int V, unsigned a, int lp) {
+  unsigned code = 0;
+  for (int r = 0; r < (1 << lp); ++r) code |= ((8u - ((a + 3u * unsigned(V) * unsigned(r)) & 7u)) & 7u) << (4 * r);
+  return code;
 }
 
 // f16x3 precision mode (mano_kernels_h3.hip): every fp32 operand x is carried
@@ -162,6 +187,8 @@ constexpr int kH3WeightExp = 14;                     // weights x 16384 (|W| <= 
 // f16 bits in the kernels' fragment layouts; see DeviceModel for each).
 struct HostModel {
   std::vector<float> tiles;     // blend_kernel B fragments [n_col_tiles][kKGroups][64][4]
+  std::vector<float> tiles_v;   // their sector-aligned variants [kAlignVariants][n_col_tiles][...]
+                                //   (empty when some variant does not fit V)
   std::vector<float> b16;       // blend_skin16 B fragments [n_groups16][3][kTile16Floats]
   std::vector<float> w16;       // LBS weight fragments [n_groups16][kWFrag16Floats]
   std::vector<float> b16v;      // sector-aligned variants [kAlignVariants][n_groups16][3][kTile16Floats]

@@ -105,24 +105,37 @@ bool pack_model(int n_verts, const double* mesh_template, const double* mesh_sha
 
   // ---- blend basis as MFMA B-fragment tiles ----
   // tile t, group g, lane l, slot q  <-  Basis[k = 2(4g+q) + (l>>5)][col = 32t + (l&31)]
-  std::vector<float> tiles(size_t(n_col_tiles) * kTileFloats, 0.f);
-  for (int t = 0; t < n_col_tiles; ++t)
-    for (int g = 0; g < kKGroups; ++g)
-      for (int l = 0; l < 64; ++l)
-        for (int q = 0; q < 4; ++q) {
-          const int k = 2 * (4 * g + q) + (l >> 5);
-          const int col = t * kColTile + (l & 31);
-          float v = 0.f;
-          if (col < n_cols) {
-            if (k < kShape)
-              v = float(mesh_shape_basis[size_t(col) * kShape + k]);
-            else if (k < kK)
-              v = float(mesh_pose_basis[size_t(col) * kPoseFeats + (k - kShape)]);
-            else if (k == kK)
-              v = float(mesh_template[col]);  // multiplied by X[:, 145] = 1
+  auto fill_tiles = [&](auto col_of, float* tiles) {
+    for (int t = 0; t < n_col_tiles; ++t)
+      for (int g = 0; g < kKGroups; ++g)
+        for (int l = 0; l < 64; ++l)
+          for (int q = 0; q < 4; ++q) {
+            const int k = 2 * (4 * g + q) + (l >> 5);
+            const int col = col_of(t, l & 31);
+            float v = 0.f;
+            if (col < n_cols) {
+              if (k < kShape)
+                v = float(mesh_shape_basis[size_t(col) * kShape + k]);
+              else if (k < kK)
+                v = float(mesh_pose_basis[size_t(col) * kPoseFeats + (k - kShape)]);
+              else if (k == kK)
+                v = float(mesh_template[col]);  // multiplied by X[:, 145] = 1
+            }
+            tiles[((size_t(t) * kKGroups + g) * 64 + l) * 4 + q] = v;
           }
-          tiles[((size_t(t) * kKGroups + g) * 64 + l) * 4 + q] = v;
-        }
+  };
+  std::vector<float> tiles(size_t(n_col_tiles) * kTileFloats, 0.f);
+  fill_tiles([&](int t, int j) { return t * kColTile + j; }, tiles.data());
+  // ... and their sector-aligned variants (mano_layout.h aligned_tile_col)
+  bool col_variants_ok = true;
+  for (int sg = 0; sg < kAlignVariants; ++sg)
+    col_variants_ok = col_variants_ok && aligned_col_variant_ok(n_cols, sg, n_col_tiles);
+  std::vector<float> tiles_v;
+  if (col_variants_ok) {
+    tiles_v.assign(size_t(kAlignVariants) * tiles.size(), 0.f);
+    for (int sg = 0; sg < kAlignVariants; ++sg)
+      fill_tiles([&](int t, int j) { return aligned_tile_col(n_cols, sg, t, j); }, tiles_v.data() + sg * tiles.size());
+  }
   // 16x16x4 fused layout: group g = 16 vertices from min(16g, V-16); and
   // the sector-aligned variants (mano_layout.h aligned_group_vertex).
   const int n_groups16 = (V + 15) / 16;
@@ -211,6 +224,7 @@ bool pack_model(int n_verts, const double* mesh_template, const double* mesh_sha
 
 
   out.tiles = std::move(tiles);
+  out.tiles_v = std::move(tiles_v);
   out.b16 = std::move(b16);
   out.w16 = std::move(w16);
   out.b16v = std::move(b16v);

@@ -79,6 +79,35 @@ void check_mesh(int V, uint64_t seed) {
           const float got = hm.tiles[((size_t(t) * kKGroups + g) * 64 + l) * 4 + q];
           EXPECT(got == want, "V=%d tile %d g %d l %d q %d: %g vs %g", V, t, g, l, q, got, want);
         }
+  // the blend tiles' sector-aligned variants: present iff every sigma fits;
+  // variant sigma tile t lane j holds aligned_tile_col's column (zero past
+  // the row end); every column is covered exactly once; for a row at float
+  // phase c the tiles t < ta of variant (8 - c) mod 8 start on a sector
+  bool cols_ok = true;
+  for (int sg = 0; sg < kAlignVariants; ++sg) cols_ok = cols_ok && aligned_col_variant_ok(n_cols, sg, hm.n_col_tiles);
+  EXPECT(cols_ok == !hm.tiles_v.empty(), "V=%d column variants present %d", V, int(cols_ok));
+  if (V == 778) EXPECT(cols_ok, "V=778 must have every column variant");
+  for (int sg = 0; sg < kAlignVariants && !hm.tiles_v.empty(); ++sg) {
+    std::vector<int> cnt(n_cols, 0);
+    for (int t = 0; t < hm.n_col_tiles; ++t)
+      for (int l = 0; l < 64; ++l) {
+        const int col = aligned_tile_col(n_cols, sg, t, l & 31);
+        if (l < 32 && col < n_cols) ++cnt[col];
+        if (t < (n_cols - sg) / 32 && l == 0) EXPECT((unsigned(col) + 8u - unsigned(sg)) % 8 == 0, "col phase");
+        for (int g = 0; g < kKGroups; ++g)
+          for (int q = 0; q < 4; ++q) {
+            const int k = 2 * (4 * g + q) + (l >> 5);
+            const float want = col < n_cols ? float(basis(k, col)) : 0.f;
+            EXPECT(hm.tiles_v[(((size_t(sg) * hm.n_col_tiles + t) * kKGroups + g) * 64 + l) * 4 + q] == want,
+                   "V=%d tiles_v s %d t %d l %d k %d", V, sg, t, l, k);
+          }
+      }
+    for (int c = 0; c < n_cols; ++c) EXPECT(cnt[c] == 1, "V=%d sigma %d column %d covered %d times", V, sg, c, cnt[c]);
+  }
+  for (unsigned phase = 0; phase < 8; ++phase) {
+    const int sg = int(aligned_col_shifts(V, phase, 0) & 15u);
+    EXPECT((phase + unsigned(sg)) % 8 == 0, "V=%d column shift of phase %u", V, phase);
+  }
   // blend_skin16 fragments: group g covers vertices vb..vb+15, vb = min(16g, V-16)
   EXPECT(hm.b16.size() == size_t(n_groups) * 3 * kTile16Floats && hm.w16.size() == size_t(n_groups) * 256,
          "b16/w16 size");
@@ -143,15 +172,17 @@ void check_mesh(int V, uint64_t seed) {
   // quad's rows all share one class; rows of class r sit at the phase its
   // shift aligns.
   const int lp = aligned_period_log2(V);
-  for (int64_t n : {1, 2, 3, 5, 63, 64, 65, 255, 256, 257, 511, 1000, 1027, 4097}) {
+  for (int lq : {6, 7})
+  for (int64_t n : {1, 2, 3, 5, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 1000, 1027, 4097}) {
     std::vector<int> hit(size_t(n), 0);
-    const int64_t nq = aligned_n_quads(n, lp);
+    const int64_t nq = aligned_n_quads(n, lp, lq);
+    const int T = 1 << (lq - 2);
     for (int64_t q = 0; q < nq; ++q)
       for (int wv = 0; wv < 4; ++wv) {
-        const AlignedTile t = aligned_tile(n, lp, q, wv);
-        EXPECT(t.n_valid >= 1 && t.n_valid <= 16 && t.h0 >= 0 && t.h0 < n, "V=%d n %lld q %lld w %d", V,
+        const AlignedTile t = aligned_tile(n, lp, q, wv, lq);
+        EXPECT(t.n_valid >= 1 && t.n_valid <= T && t.h0 >= 0 && t.h0 < n, "V=%d n %lld q %lld w %d", V,
                (long long)n, (long long)q, wv);
-        for (int i = 0; i < 16; ++i) {
+        for (int i = 0; i < T; ++i) {
           const int64_t h = t.h0 + (int64_t(i < t.n_valid ? i : t.n_valid - 1) << lp);
           EXPECT(h >= 0 && h < n && (h & ((1 << lp) - 1)) == t.cls, "V=%d n %lld hand %lld", V, (long long)n,
                  (long long)h);
