@@ -29,6 +29,13 @@ for s in ${STEPS:-tests align pmc bench c4}; do
           done
         done
       done ;;
+    path) step time_path 600 python tools/debug/time_path.py ${ALIGN_LIBS:-libmano_hip.so} --reps 2 ;;
+    pmcblend)
+      for lib in ${PMC_LIBS:-libmano_hip.so}; do
+        for c in WRITE_SIZE FETCH_SIZE; do
+          MANO_LIB=$lib step pmcu_${lib%.so}_$c 90 rocprofv3 --pmc $c -d $OUT/pmcu_${lib%.so}_$c -o p --output-format csv -- python tools/debug/run_path.py unfused 20
+        done
+      done ;;
     bench) step bench 400 python bench.py --steps 20 --warmup 5 ;;
     c4) step bench_c4_pg 400 python bench.py --force-pg --workload C4 --steps 20 --warmup 5 --no-extra --no-dropin --cpu-seconds 5 ;;
     *) if [ -n "${EXTRA:-}" ]; then step extra 400 bash -c "$EXTRA"; fi ;;
