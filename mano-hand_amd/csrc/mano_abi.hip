@@ -135,7 +135,7 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
 
   // ---- one device block, 256-B aligned sub-arrays ----
   struct Part { const void* src; size_t bytes; size_t off; };
-  enum { kBasis, kWeights, kJt, kJs, kParents, kDepth, kPcaB, kPcaM, kZeros, kStatus, kBasis16, kW16, kBasisH3, kB16V, kW16V, kTilesV, kNParts };
+  enum { kBasis, kWeights, kJt, kJs, kParents, kDepth, kPcaB, kPcaM, kZeros, kStatus, kBasis16, kW16, kBasisH3, kB16V, kW16V, kTilesV, kBh3V, kNParts };
   std::vector<Part> parts(kNParts);
   parts[kBasis] = {hm.tiles.data(), hm.tiles.size() * 4, 0};
   parts[kWeights] = {hm.weights.data(), hm.weights.size() * 4, 0};
@@ -153,6 +153,7 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   parts[kB16V] = {hm.b16v.data(), hm.b16v.size() * 4, 0};
   parts[kW16V] = {hm.w16v.data(), hm.w16v.size() * 4, 0};
   parts[kTilesV] = {hm.tiles_v.data(), hm.tiles_v.size() * 4, 0};
+  parts[kBh3V] = {hm.bh3v.data(), hm.bh3v.size() * 2, 0};
   size_t total = 0;
   for (auto& p : parts) {
     p.off = total;
@@ -195,6 +196,7 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   m->dm.basis16v = hm.b16v.empty() ? nullptr : at(kB16V);
   m->dm.wfrag16v = hm.w16v.empty() ? nullptr : at(kW16V);
   m->dm.basis_h3 = reinterpret_cast<uint16_t*>(at(kBasisH3));
+  m->dm.basis_h3v = hm.bh3v.empty() ? nullptr : reinterpret_cast<uint16_t*>(at(kBh3V));
   m->dm.h3_vposed_unscale = float(std::ldexp(1.0, -hm.basis_exp));
   m->dm.h3_lbs_unscale = float(std::ldexp(1.0, -(kH3FrameExp + kH3WeightExp)));
   m->dm.precision = MANO_PRECISION_FP32;

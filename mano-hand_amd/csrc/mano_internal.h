@@ -29,6 +29,7 @@ struct DeviceModel {
   float* basis16v;      // [kAlignVariants][n_groups16][3][kTile16Floats] sector-aligned variants,
   float* wfrag16v;      // [kAlignVariants][n_groups16][kWFrag16Floats]   NULL when V has none (mano_layout.h)
   uint16_t* basis_h3;   // [n_groups16][kH3GroupHalves] f16 bits (f16x3 mode)
+  uint16_t* basis_h3v;  // [kAlignVariants][n_groups16][kH3GroupHalves] sector-aligned variants (or NULL)
   float h3_vposed_unscale;  // 2^-basis_exp: GEMM accumulator -> v_posed
   float h3_lbs_unscale;     // 2^-(kH3FrameExp + kH3WeightExp): LBS sum -> verts
   int32_t precision;    // MANO_PRECISION_* of mano_forward / blend_skin / skin

@@ -121,7 +121,7 @@ __global__ __launch_bounds__(256, 2) void blend_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // A wave past the batch end recomputes the quad's last tile (identical values).
-  const AlignedTile tile = aligned_tile(n, lp, blockIdx.x, wave, 7);
+  const AlignedTile tile = aligned_tile(n, lp, blockIdx.x, wave, 7, 5);
   const int sigma = aligned ? int((shifts >> (4 * tile.cls)) & 15u) : 0;
   const float* tiles = basis_tiles + (aligned ? int64_t(sigma) * n_col_tiles * kTileFloats : 0);
 

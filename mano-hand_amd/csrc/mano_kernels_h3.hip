@@ -46,6 +46,10 @@
 #ifndef MANO_H3_ASM_MFMA
 #define MANO_H3_ASM_MFMA 0
 #endif
+// Sector-aligned output rows (mano_layout.h; diagnostic builds: 0 = plain).
+#ifndef MANO_H3_ALIGN
+#define MANO_H3_ALIGN 1
+#endif
 
 namespace mano {
 namespace {
@@ -171,10 +175,15 @@ __device__ __forceinline__ void split_frames_h3(const f32x4 (&raw)[24], int lane
   }
 }
 
+// The fused kernel's tiles: hands h0 + (i << lp), i <= rmax (rows past rmax
+// repeat hand rmax; residue-class tiles, mano_layout.h).
 __device__ __forceinline__ void load_frames_h3(const float* __restrict__ transforms, int64_t h0,
-                                               int64_t n, int lane, f16x8 (&F)[12]) {
+                                               int lp, int rmax, int lane, f16x8 (&F)[12]) {
   f32x4 raw[24];
-  fetch_frames_h3(transforms, h0, n, lane, raw);
+  const int64_t hand = h0 + (int64_t(min(lane & 15, rmax)) << lp);
+  const f32x4* A = reinterpret_cast<const f32x4*>(transforms + hand * kTransformFloats) + 8 * ((lane >> 4) & 1) * 3;
+#pragma unroll
+  for (int i = 0; i < 24; ++i) raw[i] = A[i];
   split_frames_h3(raw, lane, F);
 }
 
@@ -292,15 +301,18 @@ __global__ __launch_bounds__(64 * kH3Waves, kH3BlocksPerCU) void blend_skin_h3_k
     const float* __restrict__ features, const float* __restrict__ transforms,
     const uint16_t* __restrict__ basis_h3, const float* __restrict__ trans,
     float* __restrict__ verts, float* __restrict__ vposed, int64_t n, int n_verts, int n_groups,
-    float p_unscale, float t_unscale) {
+    float p_unscale, float t_unscale, int lp, unsigned shifts, int aligned) {
   constexpr int kSlot = kH3GroupPieces * 64;                // f16x8 per slot (32 KB)
   constexpr int kStores = (MANO_H3_ABLATE & 2) ? 0 : (kVposed ? 8 : 4) * kH3TPW;  // global_store_dwordx3 per group
   constexpr int kTiles = kH3Waves * kH3TPW;                 // hand tiles per block unit
   __shared__ f16x8 ring[2 * kSlot];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  static_assert(kTiles == 8, "residue-class sets of 8 16-hand tiles (mano_layout.h, lq = 7)");
   const int vstride = 3 * n_verts;
-  const int64_t nt16 = (n + 15) / 16;
-  const int64_t n_sets = (nt16 + kTiles - 1) / kTiles;
+  const int rstride = vstride << lp;  // floats between a tile's rows
+  // Sector-aligned rows (mano_layout.h, as blend_skin16): a set holds the 128
+  // hands of one residue class r, and the block uses basis variant s_r.
+  const int64_t n_sets = aligned_n_quads(n, lp, 7);
   int64_t u, u_end;
   unit_range_h3(n_sets * n_groups, blockIdx.x, gridDim.x, u, u_end);
 
@@ -315,7 +327,10 @@ __global__ __launch_bounds__(64 * kH3Waves, kH3BlocksPerCU) void blend_skin_h3_k
     const int q = lane >> 4;
     const int col = lane & 15;
 
-    stage_group_h3(basis_h3, g0, ring, wave, lane);
+    const AlignedTile tile = aligned_tile(n, lp, set, wave, 7, 4);
+    const int shift = aligned ? int((shifts >> (4 * tile.cls)) & 15u) : 0;
+    const uint16_t* bvar = basis_h3 + (aligned ? int64_t(shift) * n_groups * kH3GroupHalves : 0);
+    stage_group_h3(bvar, g0, ring, wave, lane);
     f16x8 xh[kH3TPW][kH3Steps], xl[kH3TPW][kH3Steps], F[kH3TPW][12];
     float tr[kH3TPW][4][3] = {};
     unsigned roff[kH3TPW][4];  // D rows (hands 4q + r) of each tile, clamped to the batch
@@ -323,21 +338,22 @@ __global__ __launch_bounds__(64 * kH3Waves, kH3BlocksPerCU) void blend_skin_h3_k
     float* ptile[kH3TPW];
 #pragma unroll
     for (int t = 0; t < kH3TPW; ++t) {
-      // A tile past the batch end recomputes the last tile (identical values).
-      const int64_t h0 = min(set * kTiles + wave * kH3TPW + t, nt16 - 1) * 16;
-      const int rmax = int(n - 1 - h0 < 15 ? n - 1 - h0 : 15);  // last row of the tile in the batch
-      load_x_h3(features + (h0 + min(col, rmax)) * kXStride, q, xh[t], xl[t]);
-      load_frames_h3(transforms, h0, n, lane, F[t]);
+      // A tile past the batch end recomputes the set's last tile (identical
+      // values).  The tile's rows are hands h0 + (i << lp), i <= rmax.
+      const int64_t h0 = tile.h0;
+      const int rmax = tile.n_valid - 1;  // last row of the tile in the batch
+      load_x_h3(features + (h0 + (int64_t(min(col, rmax)) << lp)) * kXStride, q, xh[t], xl[t]);
+      load_frames_h3(transforms, h0, lp, rmax, lane, F[t]);
       operand_fence(xh[t]);
       operand_fence(xl[t]);
       operand_fence(F[t]);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int hr = min(4 * q + r, rmax);
-        roff[t][r] = unsigned(hr * vstride + 3 * col);
+        roff[t][r] = unsigned(hr * rstride);
         if constexpr (kTrans) {
 #pragma unroll
-          for (int c = 0; c < 3; ++c) tr[t][r][c] = trans[(h0 + hr) * 3 + c];
+          for (int c = 0; c < 3; ++c) tr[t][r][c] = trans[(h0 + (int64_t(hr) << lp)) * 3 + c];
         }
       }
       vtile[t] = verts + h0 * int64_t(vstride);
@@ -349,7 +365,7 @@ __global__ __launch_bounds__(64 * kH3Waves, kH3BlocksPerCU) void blend_skin_h3_k
     for (int grp = g0, slot = 0; grp < g1; ++grp, slot ^= 1) {
       if (!(MANO_H3_ABLATE & 8) && grp + 1 < g1) {
         if constexpr (MANO_H3_DMA_PRIO != 0) __builtin_amdgcn_s_setprio(MANO_H3_DMA_PRIO);
-        stage_group_h3(basis_h3, grp + 1, ring + (slot ^ 1) * kSlot, wave, lane);
+        stage_group_h3(bvar, grp + 1, ring + (slot ^ 1) * kSlot, wave, lane);
         if constexpr (MANO_H3_DMA_PRIO != 0) __builtin_amdgcn_s_setprio(0);
       }
       const f16x8* L = ring + slot * kSlot + lane;
@@ -386,7 +402,14 @@ __global__ __launch_bounds__(64 * kH3Waves, kH3BlocksPerCU) void blend_skin_h3_k
 #pragma unroll
           for (int t = 0; t < kH3TPW; ++t) mfma_acc(p[t][c], xh[t][s], b);
         }
-      const int voff = 3 * min(grp * 16, n_verts - 16);
+      // the lane's vertex in this group (grp, shift uniform: scalar branches)
+      int vx;
+      if (aligned) {
+        vx = aligned_group_vertex(n_verts, shift, grp, col);
+      } else {
+        vx = (grp * 16 < n_verts - 16 ? grp * 16 : n_verts - 16) + col;
+      }
+      const int voff = 3 * vx;
       const f16x8 w1 = L[kH3WPiece * 64];
       const f16x8 w2 = L[(kH3WPiece + 1) * 64];
 #pragma unroll
@@ -405,13 +428,13 @@ __global__ __launch_bounds__(64 * kH3Waves, kH3BlocksPerCU) void blend_skin_h3_k
           lbs_h3(F[t], w1, w2, p[t], t_unscale, tr[t], out);
         }
         if constexpr (MANO_H3_ABLATE & 2) {
-          if (out[0][0] == 1234.5f && out[1][1] == 2345.5f) vtile[t][roff[t][0] + voff] = out[2][2];
+          if (out[0][0] == 1234.5f && out[1][1] == 2345.5f) vtile[t][roff[t][0] + unsigned(voff)] = out[2][2];
           continue;
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          store_out_h3(vtile[t] + (roff[t][r] + voff), f32x3{out[0][r], out[1][r], out[2][r]});
-          if constexpr (kVposed) store_out_h3(ptile[t] + (roff[t][r] + voff), f32x3{p[t][0][r], p[t][1][r], p[t][2][r]});
+          store_out_h3(vtile[t] + (roff[t][r] + unsigned(voff)), f32x3{out[0][r], out[1][r], out[2][r]});
+          if constexpr (kVposed) store_out_h3(ptile[t] + (roff[t][r] + unsigned(voff)), f32x3{p[t][0][r], p[t][1][r], p[t][2][r]});
         }
       }
       // Group grp + 1 has landed in LDS (every wave's pieces) and every wave
@@ -521,11 +544,22 @@ dim3 persistent_grid_h3(Kernel kernel, const DeviceModel& m, int64_t units, int 
 hipError_t launch_blend_skin_h3(const DeviceModel& m, int64_t n, const float* features,
                                 const float* transforms, const float* trans, float* verts,
                                 float* vposed, hipStream_t stream) {
-  const int64_t units = ((n + 15) / 16 + kH3Waves * kH3TPW - 1) / (kH3Waves * kH3TPW) * m.n_groups16;
+  // Sector-aligned rows as launch_blend_skin (mano_layout.h): verts phase
+  // classes and the basis variant of each (MANO_H3_ALIGN 0: the plain layout).
+  int lp = 0, aligned = 0;
+  unsigned shifts = 0;
+  const uint16_t* bh3 = m.basis_h3;
+  if (MANO_H3_ALIGN && m.basis_h3v) {
+    lp = aligned_period_log2(m.n_verts);
+    shifts = aligned_shifts(m.n_verts, unsigned(reinterpret_cast<uintptr_t>(verts) >> 2) & 7u, lp);
+    bh3 = m.basis_h3v;
+    aligned = 1;
+  }
+  const int64_t units = aligned_n_quads(n, lp, 7) * m.n_groups16;
   auto launch = [&](auto kernel) {
     hipLaunchKernelGGL(kernel, persistent_grid_h3(kernel, m, units, 1, kBlendSkinH3BlocksPerCU, 64 * kH3Waves),
-                       dim3(64 * kH3Waves), 0, stream, features, transforms, m.basis_h3, trans, verts, vposed,
-                       n, m.n_verts, m.n_groups16, m.h3_vposed_unscale, m.h3_lbs_unscale);
+                       dim3(64 * kH3Waves), 0, stream, features, transforms, bh3, trans, verts, vposed,
+                       n, m.n_verts, m.n_groups16, m.h3_vposed_unscale, m.h3_lbs_unscale, lp, shifts, aligned);
   };
   if (trans && vposed) launch(blend_skin_h3_kernel<true, true>);
   else if (trans) launch(blend_skin_h3_kernel<true, false>);

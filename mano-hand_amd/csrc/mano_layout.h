@@ -104,8 +104,9 @@ constexpr unsigned aligned_shifts(int V, unsigned a, int lp) {
 // The hand tiles of the kernels that use the variants, in residue classes
 // (P = 2^lp; lp = 0 is the plain layout): a block's quad (r, j) holds the
 // 2^lq hands 2^lq P j + P i + r, i < 2^lq, wave w of the block the tile of
-// T = 2^(lq - 2) hands with i = T w .. T w + T - 1 (blend_skin16: lq = 6, 16-hand
-// tiles; blend: lq = 7, 32-hand tiles).  Quads are numbered class-major.
+// T = 2^lt hands with i = T w .. T w + T - 1 (blend_skin16: lq = 6, lt = 4, 4
+// waves; blend: lq = 7, lt = 5, 4 waves; blend_skin_h3: lq = 7, lt = 4, 8
+// waves).  Quads are numbered class-major.
 __host__ __device__ inline int64_t aligned_class_quads(int64_t n, int lp, int r, int lq = 6) {
   return n > r ? ((n - 1 - r) >> (lq + lp)) + 1 : 0;
 }
@@ -123,8 +124,8 @@ struct AlignedTile {
   int n_valid;
   int cls;
 };
-__host__ __device__ inline AlignedTile aligned_tile(int64_t n, int lp, int64_t quad, int wave, int lq = 6) {
-  const int lt = lq - 2;  // log2 of the tile's hands
+__host__ __device__ inline AlignedTile aligned_tile(int64_t n, int lp, int64_t quad, int wave, int lq = 6,
+                                                   int lt = 4) {
   int cls = 0;
   int64_t j = quad;
   while (cls + 1 < (1 << lp) && j >= aligned_class_quads(n, lp, cls, lq))
@@ -195,6 +196,7 @@ struct HostModel {
   std::vector<float> w16v;      //   and their W fragments [kAlignVariants][n_groups16][kWFrag16Floats]
                                 //   (empty when some variant does not fit V)
   std::vector<uint16_t> bh3;    // f16x3 pieces [n_groups16][kH3GroupHalves]
+  std::vector<uint16_t> bh3v;   // their sector-aligned variants [kAlignVariants][n_groups16][...]
   std::vector<float> weights;   // [V][16]
   std::vector<float> jt, js;    // J_regressor . template [16][3], . shapedirs [16][3][10]
   std::vector<float> pca, pmean;  // [45][45], [45] (zeros without PCA arrays)

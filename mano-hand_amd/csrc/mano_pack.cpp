@@ -184,35 +184,43 @@ bool pack_model(int n_verts, const double* mesh_template, const double* mesh_sha
   for (size_t i = 0; i < size_t(V) * 3; ++i) bmax = std::max(bmax, std::fabs(mesh_template[i]));
   const int basis_exp = bmax > 0.0 ? 14 - int(std::ceil(std::log2(bmax))) : 0;
   const double bscale = std::ldexp(1.0, basis_exp), wscale = std::ldexp(1.0, kH3WeightExp);
-  std::vector<uint16_t> bh3(size_t(n_groups16) * kH3GroupHalves, 0);
-  for (int g = 0; g < n_groups16; ++g) {
-    const int vb = std::max(0, std::min(16 * g, V - 16));
-    uint16_t* G = bh3.data() + size_t(g) * kH3GroupHalves;
-    for (int l = 0; l < 64; ++l) {
-      const int v = vb + (l & 15);
-      for (int j = 0; j < 8; ++j) {
-        const int kq = 8 * (l >> 4) + j;  // K index inside a 32-step
-        for (int c = 0; c < 3; ++c)
-          for (int s = 0; s < kH3Steps; ++s) {
-            const int k = 32 * s + kq;
-            double val = 0.0;
-            if (k <= kK && v < V) {
-              const size_t colv = size_t(v) * 3 + c;
-              val = k < kShape ? mesh_shape_basis[colv * kShape + k]
-                    : k < kK   ? mesh_pose_basis[colv * kPoseFeats + (k - kShape)]
-                               : mesh_template[colv];
+  auto fill_h3 = [&](auto vertex_of, uint16_t* bh3) {
+    for (int g = 0; g < n_groups16; ++g) {
+      uint16_t* G = bh3 + size_t(g) * kH3GroupHalves;
+      for (int l = 0; l < 64; ++l) {
+        const int v = vertex_of(g, l & 15);
+        for (int j = 0; j < 8; ++j) {
+          const int kq = 8 * (l >> 4) + j;  // K index inside a 32-step
+          for (int c = 0; c < 3; ++c)
+            for (int s = 0; s < kH3Steps; ++s) {
+              const int k = 32 * s + kq;
+              double val = 0.0;
+              if (k <= kK && v < V) {
+                const size_t colv = size_t(v) * 3 + c;
+                val = k < kShape ? mesh_shape_basis[colv * kShape + k]
+                      : k < kK   ? mesh_pose_basis[colv * kPoseFeats + (k - kShape)]
+                                 : mesh_template[colv];
+              }
+              uint16_t hi, lo;
+              split_f16(val * bscale, hi, lo);
+              G[(size_t((2 * c) * kH3Steps + s) * 64 + l) * 8 + j] = hi;
+              G[(size_t((2 * c + 1) * kH3Steps + s) * 64 + l) * 8 + j] = lo;
             }
-            uint16_t hi, lo;
-            split_f16(val * bscale, hi, lo);
-            G[(size_t((2 * c) * kH3Steps + s) * 64 + l) * 8 + j] = hi;
-            G[(size_t((2 * c + 1) * kH3Steps + s) * 64 + l) * 8 + j] = lo;
-          }
-        uint16_t hi, lo;
-        split_f16(skinning_weights[size_t(v) * kJoints + (kq & 15)] * wscale, hi, lo);
-        G[(size_t(kH3WPiece) * 64 + l) * 8 + j] = hi;                       // [Wh ; Wh]
-        G[(size_t(kH3WPiece + 1) * 64 + l) * 8 + j] = kq < 16 ? lo : 0;     // [Wl ; 0]
+          uint16_t hi, lo;
+          split_f16(skinning_weights[size_t(v) * kJoints + (kq & 15)] * wscale, hi, lo);
+          G[(size_t(kH3WPiece) * 64 + l) * 8 + j] = hi;                       // [Wh ; Wh]
+          G[(size_t(kH3WPiece + 1) * 64 + l) * 8 + j] = kq < 16 ? lo : 0;     // [Wl ; 0]
+        }
       }
     }
+  };
+  std::vector<uint16_t> bh3(size_t(n_groups16) * kH3GroupHalves, 0);
+  fill_h3([&](int g, int col) { return std::max(0, std::min(16 * g, V - 16)) + col; }, bh3.data());
+  std::vector<uint16_t> bh3v;
+  if (variants_ok) {
+    bh3v.assign(size_t(kAlignVariants) * bh3.size(), 0);
+    for (int sh = 0; sh < kAlignVariants; ++sh)
+      fill_h3([&](int g, int col) { return aligned_group_vertex(V, sh, g, col); }, bh3v.data() + sh * bh3.size());
   }
   std::vector<float> wts(size_t(V) * kJoints);
   for (size_t i = 0; i < wts.size(); ++i) wts[i] = float(skinning_weights[i]);
@@ -230,6 +238,7 @@ bool pack_model(int n_verts, const double* mesh_template, const double* mesh_sha
   out.b16v = std::move(b16v);
   out.w16v = std::move(w16v);
   out.bh3 = std::move(bh3);
+  out.bh3v = std::move(bh3v);
   out.weights = std::move(wts);
   out.jt = std::move(jt);
   out.js = std::move(js);

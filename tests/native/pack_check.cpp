@@ -172,14 +172,16 @@ void check_mesh(int V, uint64_t seed) {
   // quad's rows all share one class; rows of class r sit at the phase its
   // shift aligns.
   const int lp = aligned_period_log2(V);
-  for (int lq : {6, 7})
+  const int kGeom[3][3] = {{6, 4, 4}, {7, 5, 4}, {7, 4, 8}};  // lq, lt, waves: blend_skin16, blend, blend_skin_h3
+  for (const auto& geo : kGeom)
   for (int64_t n : {1, 2, 3, 5, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 1000, 1027, 4097}) {
+    const int lq = geo[0], lt = geo[1], waves = geo[2];
     std::vector<int> hit(size_t(n), 0);
     const int64_t nq = aligned_n_quads(n, lp, lq);
-    const int T = 1 << (lq - 2);
+    const int T = 1 << lt;
     for (int64_t q = 0; q < nq; ++q)
-      for (int wv = 0; wv < 4; ++wv) {
-        const AlignedTile t = aligned_tile(n, lp, q, wv, lq);
+      for (int wv = 0; wv < waves; ++wv) {
+        const AlignedTile t = aligned_tile(n, lp, q, wv, lq, lt);
         EXPECT(t.n_valid >= 1 && t.n_valid <= T && t.h0 >= 0 && t.h0 < n, "V=%d n %lld q %lld w %d", V,
                (long long)n, (long long)q, wv);
         for (int i = 0; i < T; ++i) {
@@ -231,6 +233,32 @@ void check_mesh(int V, uint64_t seed) {
     }
   }
   EXPECT(hm.bh3.size() > 0 && std::ldexp(1.0, 14 - hm.basis_exp) >= 5e-3, "basis_exp %d", hm.basis_exp);
+  // f16x3 sector-aligned variants: present with the fp32 ones; piece entries
+  // of variant s decode to aligned_group_vertex's vertex
+  EXPECT(hm.bh3v.empty() == hm.b16v.empty() && (hm.bh3v.empty() || hm.bh3v.size() == kAlignVariants * hm.bh3.size()),
+         "V=%d bh3v size %zu", V, hm.bh3v.size());
+  for (int sh = 0; sh < kAlignVariants && !hm.bh3v.empty(); ++sh)
+    for (int g = 0; g < n_groups; ++g) {
+      const uint16_t* G = hm.bh3v.data() + (size_t(sh) * n_groups + g) * kH3GroupHalves;
+      for (int l = 0; l < 64; ++l) {
+        const int v = aligned_group_vertex(V, sh, g, l & 15);
+        for (int j = 0; j < 8; ++j) {
+          const int kq = 8 * (l >> 4) + j;
+          for (int c = 0; c < 3; ++c)
+            for (int st = 0; st < kH3Steps; ++st) {
+              const int k = 32 * st + kq;
+              const double x = (k <= kK ? basis(k, 3 * v + c) : 0.0) * bscale;
+              const double hi = f16_value(G[(size_t((2 * c) * kH3Steps + st) * 64 + l) * 8 + j]);
+              const double lo = f16_value(G[(size_t((2 * c + 1) * kH3Steps + st) * 64 + l) * 8 + j]);
+              EXPECT(std::fabs(hi + lo - x) <= std::ldexp(std::fabs(x), -21) + std::ldexp(1.0, -24),
+                     "V=%d bh3v s %d g %d k %d", V, sh, g, k);
+            }
+          const double wx = w[size_t(v) * kJoints + (kq & 15)] * wscale;
+          EXPECT(f16_value(G[(size_t(kH3WPiece) * 64 + l) * 8 + j]) == f16_value(f16_bits(float(wx))),
+                 "V=%d bh3v Wh s %d g %d", V, sh, g);
+        }
+      }
+    }
   // J folds in float64 (mano_np.py:83)
   for (int j = 0; j < kJoints; ++j)
     for (int c = 0; c < 3; ++c) {

@@ -475,12 +475,22 @@ def test_forward_equals_staged(engine, dev, params, B, shared, with_trans):
     assert np.abs(host(one["joints"]) - ref["joints"]).max() <= TOL_M
 
 
+@pytest.mark.parametrize("precision", ["fp32", "f16x3"])
 @pytest.mark.parametrize("B", [1, 5, 64, 257, 1027])
-def test_output_phase_independent(engine, dev, params, B):
-    """blend_skin16 picks its sector-aligned operand variants (mano_layout.h)
-    from the verts address: verts / rest_verts written at every 4-B phase of a
-    32-B sector (views offset by 0..7 floats) are bit-identical to the plain
-    outputs, with and without translation, and to the oracle."""
+def test_output_phase_independent(engine, dev, params, B, precision):
+    """blend_skin16 / blend_skin_h3 pick their sector-aligned operand
+    variants (mano_layout.h) from the verts address: verts / rest_verts written
+    at every 4-B phase of a 32-B sector (views offset by 0..7 floats) are
+    bit-identical to the plain outputs, with and without translation, and to
+    the oracle."""
+    engine.set_precision(precision)
+    try:
+        _phase_check(engine, dev, params, B)
+    finally:
+        engine.set_precision("fp32")
+
+
+def _phase_check(engine, dev, params, B):
     rng = np.random.default_rng(900 + B)
     betas = f32(rng.normal(0, 1, (B, 10)), dev)
     pose = f32(rng.normal(0, 0.5, (B, 16, 3)), dev)
