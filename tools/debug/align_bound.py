@@ -93,6 +93,14 @@ res["verts_digest"] = digest(ref_layout(v))
 res["blend_skin_b2b"] = steps([lambda: m.stage_blend_skin(B, v)])[0]
 res["blend_skin_rest_verts"] = steps([lambda: m.stage_blend_skin(B, v, rest_verts=vp)])[0]
 res["rest_digest"] = [digest(ref_layout(v)), digest(ref_layout(vp))]
+if not scratch:   # the f16x3 fused kernel (blend_skin_h3) the same way
+    m.set_precision("f16x3")
+    a, f = steps([art, lambda: m.stage_blend_skin(B, v)])
+    res["h3_fused"] = {"articulate": a, "blend_skin": f, "step": a + f}
+    res["h3_verts_digest"] = digest(ref_layout(v))
+    res["h3_rest_verts"] = steps([lambda: m.stage_blend_skin(B, v, rest_verts=vp)])[0]
+    res["h3_rest_digest"] = [digest(ref_layout(v)), digest(ref_layout(vp))]
+    m.set_precision("fp32")
 res["status"] = m.device_status()
 print("RESULT " + json.dumps(res), flush=True)
 '''
