@@ -77,6 +77,9 @@ __device__ __forceinline__ f32x16 mfma_tile(const float (&a)[kKGroups * 4], cons
 // h0 + (hr << lp), hr < n_valid (residue-class tiles, mano_layout.h); rows
 // past n_valid and columns past the row end fall outside the buffer and are
 // dropped.
+#ifndef MANO_BLEND_STORE_POLICY
+#define MANO_BLEND_STORE_POLICY 1  // buffer-store cache policy bits of v_posed (1 = sc0; diagnostic builds: others)
+#endif
 __device__ __forceinline__ void store_vposed_tile(float* __restrict__ vposed, const f32x16& acc,
                                                   int64_t h0, int lp, int n_valid, int col, int n_cols,
                                                   int hi) {
@@ -89,7 +92,7 @@ __device__ __forceinline__ void store_vposed_tile(float* __restrict__ vposed, co
     for (int r = 0; r < 16; ++r) {
       const int hr = (r & 3) + 8 * (r >> 2) + 4 * hi;
       const float x = acc[r];  // a scalar first: __builtin_bit_cast of a vector element reads element 0
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), rs, 4 * (hr * rstride + col), 0, 1 /* sc0 */);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), rs, 4 * (hr * rstride + col), 0, MANO_BLEND_STORE_POLICY);
     }
   }
 }
@@ -361,6 +364,11 @@ __device__ __forceinline__ void bs_barrier() {
 #ifndef MANO_BS_NT_STORE
 #define MANO_BS_NT_STORE 1
 #endif
+// With rest_verts (diagnostic builds): bit 0 = verts nontemporal, bit 1 =
+// rest_verts nontemporal (round 3, with partial sectors: 0 was best).
+#ifndef MANO_BS_REST_NT
+#define MANO_BS_REST_NT 0
+#endif
 __device__ __forceinline__ float* byte_at(float* base, unsigned byte_off) {
   return reinterpret_cast<float*>(reinterpret_cast<char*>(base) + byte_off);
 }
@@ -427,8 +435,8 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
   // nontemporal only with one output stream (beside the rest_verts stream
   // either one nontemporal took 0.71 vs 0.61 ms, both 0.86:
   // profiles/r03m_ab_rest_nt.jsonl)
-  constexpr bool kVertsNt = MANO_BS_NT_STORE && !kVposed;
-  constexpr bool kRestNt = false;
+  constexpr bool kVertsNt = kVposed ? bool(MANO_BS_REST_NT & 1) : bool(MANO_BS_NT_STORE);
+  constexpr bool kRestNt = MANO_BS_REST_NT & 2;
   constexpr int kDeferAt = 2;
   __shared__ f32x4 lds[kSlots * kRingF4];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

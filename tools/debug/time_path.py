@@ -84,6 +84,12 @@ def main():
         reps = int(args[i + 1])
         del args[i:i + 2]
     libs = args or ["libmano_hip.so"]
+    # MANO_BS_ABLATE=4 builds write verts in a larger scratch layout
+    # (n x n_groups x 256 B, tools/debug/align_bound.py): this tool's
+    # reference-layout buffers are too small for them (out-of-bounds writes)
+    bad = [l for l in libs if "abl4" in l]
+    if bad:
+        raise SystemExit(f"time_path.py cannot run scratch-layout builds {bad}: use align_bound.py")
     for rep in range(reps):
         for lib in libs:
             r = subprocess.run([sys.executable, "-c", CHILD, REPO, lib], capture_output=True, text=True,

@@ -29,7 +29,7 @@ for s in ${STEPS:-tests align pmc bench c4}; do
           done
         done
       done ;;
-    path) step time_path 600 python tools/debug/time_path.py ${ALIGN_LIBS:-libmano_hip.so} --reps 2 ;;
+    path) step time_path 600 python tools/debug/time_path.py ${PATH_LIBS:-libmano_hip.so} --reps 2 ;;
     pmcblend)
       for lib in ${PMC_LIBS:-libmano_hip.so}; do
         for c in WRITE_SIZE FETCH_SIZE; do
