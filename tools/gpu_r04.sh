@@ -36,6 +36,7 @@ for s in ${STEPS:-tests align pmc bench c4}; do
           MANO_LIB=$lib step pmcu_${lib%.so}_$c 90 rocprofv3 --pmc $c -d $OUT/pmcu_${lib%.so}_$c -o p --output-format csv -- python tools/debug/run_path.py unfused 20
         done
       done ;;
+    probe) step skin_align_probe 400 python tools/debug/skin_align_probe.py --reps 2 ;;
     bench) step bench 400 python bench.py --steps 20 --warmup 5 ;;
     c4) step bench_c4_pg 400 python bench.py --force-pg --workload C4 --steps 20 --warmup 5 --no-extra --no-dropin --cpu-seconds 5 ;;
     *) if [ -n "${EXTRA:-}" ]; then step extra 400 bash -c "$EXTRA"; fi ;;
