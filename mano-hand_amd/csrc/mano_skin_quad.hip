@@ -564,21 +564,49 @@ struct PairStamp {
 
 // kH3: the f16x3 mode (skin_unit4_h3, W halves from basis_h3's pieces 30 /
 // 31, t_unscale); otherwise fp32 (wfrag16).
-template <bool kTrans, bool kH3 = false>
+//
+// kAlign (fp32): sector-aligned units (mano_layout.h).  A unit's 4 hands are
+// of one residue class of the rows' 32-B sector phase (hands c + P (4 q + r),
+// P = 2^lp), blocks are dealt to the classes round robin (block b serves
+// class b mod P), and a class's 64-vertex spans start at its shift s
+// (vertices s + 64 k), so every full span's four 768-B row segments start on
+// a sector boundary and their float4 loads and stores are 16-B aligned.  The
+// W fragments in LDS are variant s's groups 0 .. 4 n_full - 1 (wfrag16v)
+// followed by the plain first and last groups; the edge unit of a hand quad
+// stages vertices [0, 16) and [V - 16, V) side by side in its rows (24
+// float4 per row, lanes 0-11 and 12-23 of one DMA) and skins them as two
+// groups -- the rows' first and last sectors, which neighbouring hands share
+// in any layout, and the aligned spans' edges rewritten with identical values.
+template <bool kTrans, bool kH3 = false, bool kAlign = false>
 __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     const float* __restrict__ transforms, const float* __restrict__ wfrag16,
     const float* __restrict__ vposed, const float* __restrict__ trans, float* __restrict__ verts,
     int64_t n, int n_verts, int n_groups, const uint16_t* __restrict__ basis_h3, float t_unscale,
-    int* __restrict__ status) {
+    int* __restrict__ status, const float* __restrict__ wfrag16v, int lp, unsigned shifts) {
+  static_assert(!(kAlign && kH3), "aligned units: fp32 only");
   __shared__ f32x4 w_lds[kPairMaxGroups * 64];
   __shared__ PairShared sh;
-  for (int i = threadIdx.x; i < n_groups * 64; i += 64 * kPairWaves) {
-    if constexpr (kH3) {
+  const int P = kAlign ? 1 << lp : 1;
+  const int bcls = kAlign ? int(blockIdx.x) & (P - 1) : 0;  // this block's residue class
+  const int shift = kAlign ? int((shifts >> (4 * bcls)) & 15u) : 0;
+  const int n_full = n_verts / kQVerts;
+  if constexpr (kAlign) {
+    const int n_al = 4 * n_full;  // variant groups, then the plain first and last group
+    const f32x4* wv = reinterpret_cast<const f32x4*>(wfrag16v + int64_t(shift) * n_groups * kWFrag16Floats);
+    const f32x4* wp = reinterpret_cast<const f32x4*>(wfrag16);
+    for (int i = threadIdx.x; i < (n_al + 2) * 64; i += 64 * kPairWaves) {
       const int grp = i >> 6, e = i & 63;
-      w_lds[i] = reinterpret_cast<const f32x4*>(basis_h3 + int64_t(grp) * kH3GroupHalves +
-                                                (kH3WPiece + (e >> 5)) * kH3PieceHalves)[e & 31];
-    } else {
-      w_lds[i] = reinterpret_cast<const f32x4*>(wfrag16)[i];
+      w_lds[i] = grp < n_al ? wv[i] : wp[(grp == n_al ? 0 : n_groups - 1) * 64 + e];
+    }
+  } else {
+    for (int i = threadIdx.x; i < n_groups * 64; i += 64 * kPairWaves) {
+      if constexpr (kH3) {
+        const int grp = i >> 6, e = i & 63;
+        w_lds[i] = reinterpret_cast<const f32x4*>(basis_h3 + int64_t(grp) * kH3GroupHalves +
+                                                  (kH3WPiece + (e >> 5)) * kH3PieceHalves)[e & 31];
+      } else {
+        w_lds[i] = reinterpret_cast<const f32x4*>(wfrag16)[i];
+      }
     }
   }
 
@@ -592,11 +620,14 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
   int lane = threadIdx.x & 63;
   asm volatile("" : "+v"(lane));
   const int vstride = 3 * n_verts;
-  const int n_full = n_verts / kQVerts;
+  const int rstride = vstride * P;  // floats between a unit's rows
   const int n_tail = n_groups - 4 * n_full;
-  const int spans = n_full + (n_tail > 0 ? 1 : 0);
-  const int64_t n_quads = (n + kQHands - 1) / kQHands;
-  const int64_t b = blockIdx.x, nb = gridDim.x;
+  const int spans = n_full + (kAlign || n_tail > 0 ? 1 : 0);
+  // hand quads of this block's class (all hands without kAlign)
+  const int64_t n_hands_c = kAlign ? (n > bcls ? (n - 1 - bcls) / P + 1 : 0) : n;
+  const int64_t n_quads = (n_hands_c + kQHands - 1) / kQHands;
+  const int64_t b = kAlign ? int64_t(blockIdx.x) / P : int64_t(blockIdx.x);
+  const int64_t nb = kAlign ? int64_t(gridDim.x) / P : int64_t(gridDim.x);
   const int64_t blk = (nb % 8) ? b : (b % 8) * (nb / 8) + b / 8;
   const int64_t worker = blk * kPairs + pair, n_workers = nb * kPairs;
   const int64_t step_q = n_workers / spans;
@@ -628,7 +659,11 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     // or tail_rf4 (tail) float4, so the stage keeps its padded row stride.
     // Rows and hands past the batch end fall outside num_records: their
     // loads write zeros, their stores are dropped.
-    const int tail_rf4 = 3 * (n_verts - tail_v0) / 4;
+    // the tail unit's float4 per row (kAlign: the edge unit's two 16-vertex pieces)
+    const int tail_rf4 = kAlign ? 24 : 3 * (n_verts - tail_v0) / 4;
+    // an edge-unit float4 at column tc of its staged row: head piece (tc < 48)
+    // at the row start, tail piece at vertex V - 16
+    auto edge_col = [&](int tc) { return tc < 48 ? tc : 3 * (n_verts - 16) + (tc - 48); };
     int fvo[kQF4], tvo[kQF4];                 // store sweep: global byte offsets in the unit's rows
     unsigned fso[kQF4], tso[kQF4];            // store sweep: LDS byte addresses in slot 0
     const unsigned slot0 = lds_addr(reinterpret_cast<const int*>(&sh.slot[pair][0]));
@@ -638,14 +673,34 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       const int fr = idx / kQRowF4, fc = 4 * (idx % kQRowF4);
       const int it = min(idx, kQHands * tail_rf4 - 1);
       const int tr = it / tail_rf4, tc = 4 * (it % tail_rf4);
-      fvo[i] = 4 * (fr * vstride + fc);
-      tvo[i] = 4 * (tr * vstride + tc);
+      fvo[i] = 4 * (fr * rstride + fc);
+      tvo[i] = 4 * (tr * rstride + (kAlign ? edge_col(tc) : tc));
       fso[i] = slot0 + unsigned(offsetof(PairStage, rows)) + 4u * unsigned(fr * kPStride + fc);
       tso[i] = slot0 + unsigned(offsetof(PairStage, rows)) + 4u * unsigned(tr * kPStride + tc);
     }
     int rvo[kPairRowDmas];  // DMA j: the lane's byte offset in the unit's rows
+    int evo[kPairRowDmas];  // kAlign, edge unit: head piece (lanes 0-11), tail piece (12-23)
 #pragma unroll
-    for (int j = 0; j < kPairRowDmas; ++j) rvo[j] = 4 * j * vstride + 16 * lane;
+    for (int j = 0; j < kPairRowDmas; ++j) {
+      rvo[j] = 4 * j * rstride + 16 * lane;
+      evo[j] = 4 * j * rstride + 4 * edge_col(4 * lane);
+    }
+    // transforms: lane's 16 B of sweep i (3 KB of the unit's 4 hands, each
+    // 768 B; kAlign: the hands are P rows apart), translations: lane < 12
+    int tro[kQTrF4];
+#pragma unroll
+    for (int i = 0; i < kQTrF4; ++i) {
+      const int bb = 1024 * i + 16 * lane;
+      tro[i] = (bb / 768) * P * 768 + bb % 768;
+    }
+    const int xo = 4 * ((lane / 3) * P * 3 + lane % 3);
+    // first hand and hands in the batch of hand quad fq (rows P apart)
+    auto unit_hands = [&](int64_t fq, int64_t& h0, int& valid) {
+      const int64_t qq = kPairReverse ? n_quads - 1 - fq : fq;
+      h0 = kAlign ? bcls + int64_t(P) * kQHands * qq : qq * kQHands;
+      const int64_t left = kAlign ? (n - 1 - h0) / P + 1 : n - h0;
+      valid = int(left < kQHands ? left : kQHands);
+    };
     constexpr int kRsrcFlags = 0x00020000;  // gfx9 raw buffer
     auto rsrc = [&](const float* base, int64_t floats) {
       return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, int(floats * 4), kRsrcFlags);
@@ -659,27 +714,35 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     constexpr int kTrOps = (MANO_QUAD_ABLATE & 4) ? 0 : kQTrF4;
     constexpr int kDmaOps = kPairRowDmas + kTrOps + (kTrans ? 1 : 0);
     auto dma = [&](int64_t fq, int fs, int slot) {
-      const int64_t h0 = (kPairReverse ? n_quads - 1 - fq : fq) * kQHands;
-      const int valid = int(n - h0 < kQHands ? n - h0 : kQHands);
-      const auto rv = rsrc(vposed + h0 * vstride, int64_t(valid) * vstride);
-      const auto rt = rsrc(transforms + h0 * kTransformFloats, int64_t(valid) * kTransformFloats);
+      int64_t h0;
+      int valid;
+      unit_hands(fq, h0, valid);
+      // rows / hands past the batch end are outside num_records (loads give 0)
+      const auto rv = rsrc(vposed + h0 * vstride, kAlign ? int64_t(valid - 1) * rstride + vstride : int64_t(valid) * vstride);
+      const auto rt = rsrc(transforms + h0 * kTransformFloats,
+                           kAlign ? int64_t(valid - 1) * P * kTransformFloats + kTransformFloats
+                                  : int64_t(valid) * kTransformFloats);
       const bool full = fs < n_full;
-      const int soff = 4 * 3 * (full ? kQVerts * fs : tail_v0);
+      const int soff = kAlign ? (full ? 4 * 3 * (shift + kQVerts * fs) : 0) : 4 * 3 * (full ? kQVerts * fs : tail_v0);
       const int row_f4 = full ? kQRowF4 : tail_rf4;
 #pragma unroll
-      for (int i = 0; i < kTrOps; ++i)
-        buffer_load_lds16(rt, lds_at(slot, unsigned(offsetof(PairStage, tr)) + 1024u * i), 16 * lane,
-                                       1024 * i);
+      for (int i = 0; i < kTrOps; ++i) {
+        if constexpr (kAlign)
+          buffer_load_lds16(rt, lds_at(slot, unsigned(offsetof(PairStage, tr)) + 1024u * i), tro[i], 0);
+        else
+          buffer_load_lds16(rt, lds_at(slot, unsigned(offsetof(PairStage, tr)) + 1024u * i), 16 * lane,
+                                         1024 * i);
+      }
       if constexpr (kTrans) {
-        const auto rr = rsrc(trans + h0 * 3, int64_t(valid) * 3);
+        const auto rr = rsrc(trans + h0 * 3, kAlign ? int64_t(valid - 1) * P * 3 + 3 : int64_t(valid) * 3);
         if (lane < 12)
-          buffer_load_lds4(rr, lds_at(slot, unsigned(offsetof(PairStage, trans))), 4 * lane, 0);
+          buffer_load_lds4(rr, lds_at(slot, unsigned(offsetof(PairStage, trans))), kAlign ? xo : 4 * lane, 0);
       }
 #pragma unroll
       for (int r = 0; r < kQHands; ++r)
         if (lane < row_f4)
           buffer_load_lds16(rv, lds_at(slot, unsigned(offsetof(PairStage, rows)) + 4u * r * kPStride),
-                                           rvo[r], soff);
+                                           kAlign && !full ? evo[r] : rvo[r], soff);
     };
     auto ds_read4 = [](unsigned addr) {
       return *reinterpret_cast<const __attribute__((address_space(3))) f32x4*>(uintptr_t(addr));
@@ -687,11 +750,14 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     constexpr unsigned kSlotBytes = sizeof(PairStage);
     auto store = [&](int64_t fq, int fs, unsigned slot, bool real) {
       const unsigned so = slot * kSlotBytes;
-      const int64_t h0 = (kPairReverse ? n_quads - 1 - fq : fq) * kQHands;
-      const int valid = real ? int(n - h0 < kQHands ? n - h0 : kQHands) : 0;  // 0: every store dropped
-      const auto ro = rsrc(verts + h0 * vstride, int64_t(valid) * vstride);
+      int64_t h0;
+      int valid;
+      unit_hands(fq, h0, valid);
+      // not real: num_records 0, every store dropped
+      const auto ro = rsrc(verts + h0 * vstride, !real ? 0 : kAlign ? int64_t(valid - 1) * rstride + vstride
+                                                                    : int64_t(valid) * vstride);
       const bool full = fs < n_full;
-      const int soff = 4 * 3 * (full ? kQVerts * fs : tail_v0);
+      const int soff = kAlign ? (full ? 4 * 3 * (shift + kQVerts * fs) : 0) : 4 * 3 * (full ? kQVerts * fs : tail_v0);
       f32x4 sdata[kQF4];
 #pragma unroll
       for (int i = 0; i < kQF4; ++i) sdata[i] = ds_read4((full ? fso[i] : tso[i]) + so);
@@ -850,6 +916,11 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
         const int G[4] = {4 * s, 4 * s + 1, 4 * s + 2, 4 * s + 3};
         const int lv[4] = {0, 16, 32, 48};
         skin_unit4<kTrans, 4, PairStage>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
+      } else if constexpr (kAlign) {
+        // the edge unit: vertices [0, 16) and [V - 16, V), staged side by side
+        const int G[4] = {4 * n_full, 4 * n_full + 1, 4 * n_full + 1, 4 * n_full + 1};
+        const int lv[4] = {0, 16, 16, 16};
+        skin_unit4<kTrans, 2, PairStage>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
       } else {
         int G[4], lv[4];
 #pragma unroll
@@ -879,6 +950,21 @@ extern "C" int mano_debug_pair_stamps(unsigned long long* host, int count) {
 }
 namespace mano {
 #endif
+
+// skin_pair's sector-aligned units (kAlign) for this mesh: the variants
+// exist, every shift's 64-vertex spans end inside the row with at most 16
+// vertices after them, and the W fragments (4 n_full variant groups + 2)
+// fit the block's LDS.
+#ifndef MANO_PAIR_ALIGN
+#define MANO_PAIR_ALIGN 0
+#endif
+bool pair_align_ok(const DeviceModel& m) {
+  const int V = m.n_verts, n_full = V / kQVerts;
+  if (!m.wfrag16v || V < 32 || 4 * n_full + 2 > kPairMaxGroups) return false;
+  for (int s = 0; s < kAlignVariants; ++s)
+    if (s + kQVerts * n_full > V || V - (s + kQVerts * n_full) > 16 || 4 * n_full > (V - s) / 16) return false;
+  return true;
+}
 
 bool skin_quad_supported(const DeviceModel& m) {
 #if MANO_QUAD_PAIR
@@ -915,10 +1001,34 @@ hipError_t launch_skin_quad(const DeviceModel& m, int64_t n, const float* transf
     else launch1(skin_quad_kernel<false>);
     return hipGetLastError();
   }
+  // Sector-aligned units (fp32): every class must give each memory wave at
+  // least 2 units with whole classes of blocks.
+  if (!h3 && MANO_PAIR_ALIGN && pair_align_ok(m)) {
+    const int lp = aligned_period_log2(m.n_verts), P = 1 << lp;
+    const unsigned shifts = aligned_shifts(m.n_verts, unsigned(reinterpret_cast<uintptr_t>(verts) >> 2) & 7u, lp);
+    const int spans_al = m.n_verts / kQVerts + 1;
+    int64_t units_min = -1;
+    for (int r = 0; r < P; ++r) {
+      const int64_t hands = n > r ? (n - 1 - r) / P + 1 : 0;
+      const int64_t u = (hands + kQHands - 1) / kQHands * spans_al;
+      units_min = units_min < 0 || u < units_min ? u : units_min;
+    }
+    const int64_t per_class = std::min<int64_t>(units_min / (2 * kPairs), cap / P);
+    if (per_class >= 1) {
+      auto launch_al = [&](auto kernel) {
+        hipLaunchKernelGGL(kernel, dim3(unsigned(per_class * P)), dim3(64 * kPairWaves), 0, stream, transforms,
+                           m.wfrag16, vposed, trans, verts, n, m.n_verts, m.n_groups16, m.basis_h3,
+                           m.h3_lbs_unscale, m.status, m.wfrag16v, lp, shifts);
+      };
+      if (trans) launch_al(skin_pair_kernel<true, false, true>);
+      else launch_al(skin_pair_kernel<false, false, true>);
+      return hipGetLastError();
+    }
+  }
   auto launch = [&](auto kernel) {
     hipLaunchKernelGGL(kernel, dim3(unsigned(blocks)), dim3(64 * kPairWaves), 0, stream, transforms,
                        m.wfrag16, vposed, trans, verts, n, m.n_verts, m.n_groups16, m.basis_h3,
-                       m.h3_lbs_unscale, m.status);
+                       m.h3_lbs_unscale, m.status, nullptr, 0, 0u);
   };
   if (h3) {
     if (trans) launch(skin_pair_kernel<true, true>);

@@ -49,9 +49,9 @@ def test_skin_pair_vmcnt_protocol(report):
     """skin_pair's memory wave waits with a hand-counted s_waitcnt vmcnt(N):
     on every control-flow path into that wait the disassembly must end with
     the awaited unit's DMA group, >= 3 stores, then exactly one DMA group
-    (tools/isa_scan.py), in all four instantiations."""
+    (tools/isa_scan.py), in all six instantiations."""
     pairs = report["skin_pair_vmcnt"]
-    assert len(pairs) == 4, sorted(pairs)
+    assert len(pairs) == 6, sorted(pairs)  # fp32 x trans x aligned units + f16x3 x trans
     for name, r in pairs.items():
         assert r["waits"] >= 1 and r["ok"], (name, r)
 
