@@ -506,10 +506,16 @@ def _phase_check(engine, dev, params, B):
             engine.stage_blend_skin(B, v, rest_verts=vp, trans=tr)
             v_only = torch.full((n + 8,), float("nan"), device=dev)[off:off + n].view(B, 778, 3)
             engine.stage_blend_skin(B, v_only, trans=tr)
+            # the unfused stages too (the blend GEMM's v_posed in the
+            # workspace, the standalone LBS into the offset view)
+            v_lbs = torch.full((n + 8,), float("nan"), device=dev)[off:off + n].view(B, 778, 3)
+            engine.stage_blend(B)
+            engine.stage_skin(B, v_lbs, trans=tr)
             torch.cuda.synchronize()
             assert torch.equal(v, want["verts"]), (off, tr is None)
             assert torch.equal(vp, want["rest_verts"]), (off, tr is None)
             assert torch.equal(v_only, want["verts"]), (off, tr is None)
+            assert torch.equal(v_lbs, want["verts"]), (off, tr is None, "unfused")
             assert torch.isnan(buf[:off]).all() and torch.isnan(buf[off + n:n + 32 + off]).all()
             assert torch.isnan(buf[2 * n + 32 + off:]).all()
     ref = mano_oracle.forward(params, host(betas), host(pose), host(trans))
