@@ -11,6 +11,13 @@ for p in (os.path.join(REPO, "mano-hand_amd"), REPO):
 
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
+# Diagnostic A/B runs only: MANO_TEST_LIB=<file in mano_amd/> runs the suite
+# against another build of the library (a tools/ variant).  The driver never
+# sets it; test_library_is_the_loaded_path then checks the named file loaded.
+if os.environ.get("MANO_TEST_LIB"):
+    from mano_amd import _abi as _abi_mod
+    _abi_mod.LIB_PATH = os.path.join(os.path.dirname(_abi_mod.LIB_PATH), os.environ["MANO_TEST_LIB"])
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")

@@ -97,7 +97,7 @@ def main():
             lines = [l for l in r.stdout.splitlines() if l.startswith("RESULT ")]
             if r.returncode != 0 or not lines:
                 print(json.dumps({"lib": lib, "rc": r.returncode, "err": r.stderr[-1500:]}), flush=True)
-                if r.returncode < 0 or r.returncode in (124, 134, 137, 139):
+                if r.returncode < 0 or r.returncode in (124, 134, 137, 139) or "HIP error" in r.stderr:
                     sys.exit(1)
                 continue
             d = json.loads(lines[-1][7:])

@@ -1,0 +1,35 @@
+#!/bin/bash
+# Round 4 (c): the GPU suite on the product tree, the aligned skin_pair
+# (MANO_PAIR_ALIGN=1 build) through the LBS parity tests, then the store-policy
+# and aligned-LBS A/B (tools/debug/time_path.py, digests compared there) and the
+# default bench.  Every GPU step time-limited; any failure other than a plain
+# test failure stops the script, and so does a failing variant suite (its
+# timings would be void).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${TAG:-r04c}
+mkdir -p $OUT
+export TMPDIR=/tmp
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" | tee -a $OUT/steps.log
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a $OUT/steps.log
+  tail -3 "$OUT/$name.log" | cut -c1-600
+  if grep -q "HIP error\|illegal memory access\|Memory access fault" "$OUT/$name.log"; then
+    echo "stopping: GPU error in $name"; exit 3
+  fi
+  return $rc
+}
+PYT="python -u -m pytest -v --timeout 180 --timeout-method thread"
+for s in ${STEPS:-tests pairal path bench}; do
+  case $s in
+    tests) step pytest_gpu 900 $PYT tests -m gpu || [ $? -eq 1 ] || exit 1 ;;
+    pairal) MANO_TEST_LIB=libmano_hip_pairal.so step pytest_pairal 400 $PYT tests/test_gpu_parity.py \
+              -k "standalone_lbs or phase_independent or other_mesh or fused_equals or library_is" || exit 1 ;;
+    path) step time_path 900 python tools/debug/time_path.py ${PATH_LIBS:-libmano_hip.so libmano_hip_pairal.so libmano_hip_restnt1.so libmano_hip_restnt2.so libmano_hip_restnt3.so libmano_hip_bpol0.so libmano_hip_bpol2.so} --reps 2 || exit 1 ;;
+    bench) step bench 400 python bench.py --steps 20 --warmup 5 || exit 1 ;;
+    stats) step kernel_stats 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o k --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu || exit 1 ;;
+  esac
+done
