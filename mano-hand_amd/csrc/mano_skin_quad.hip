@@ -514,11 +514,19 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 // LDS-DMA buffer loads (device-only helpers: the host pass of a kernel
 // template cannot instantiate this builtin and would silently drop the stub).
+template <int kAux = 0>
 __device__ __forceinline__ void buffer_load_lds16(__amdgpu_buffer_rsrc_t rsrc, unsigned lds_byte_addr, int voffset,
                                                   int soffset) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, reinterpret_cast<__attribute__((address_space(3))) void*>(uintptr_t(lds_byte_addr)),
-                                           16, voffset, soffset, 0, 0);
+                                           16, voffset, soffset, 0, kAux);
 }
+// Cache policy of skin_pair's v_posed row DMA (bit 0) and verts stores (bit 1):
+// set = nontemporal (diagnostic builds; the product streams with the default
+// policy -- with partial-sector rows nontemporal made no difference, round 2).
+#ifndef MANO_PAIR_NT
+#define MANO_PAIR_NT 0
+#endif
+constexpr int kPairRowAux = (MANO_PAIR_NT & 1) ? 2 : 0, kPairStoreAux = (MANO_PAIR_NT & 2) ? 2 : 0;
 __device__ __forceinline__ void buffer_load_lds4(__amdgpu_buffer_rsrc_t rsrc, unsigned lds_byte_addr, int voffset,
                                                  int soffset) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, reinterpret_cast<__attribute__((address_space(3))) void*>(uintptr_t(lds_byte_addr)),
@@ -741,8 +749,8 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
 #pragma unroll
       for (int r = 0; r < kQHands; ++r)
         if (lane < row_f4)
-          buffer_load_lds16(rv, lds_at(slot, unsigned(offsetof(PairStage, rows)) + 4u * r * kPStride),
-                                           kAlign && !full ? evo[r] : rvo[r], soff);
+          buffer_load_lds16<kPairRowAux>(rv, lds_at(slot, unsigned(offsetof(PairStage, rows)) + 4u * r * kPStride),
+                                         kAlign && !full ? evo[r] : rvo[r], soff);
     };
     auto ds_read4 = [](unsigned addr) {
       return *reinterpret_cast<const __attribute__((address_space(3))) f32x4*>(uintptr_t(addr));
@@ -764,7 +772,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
 #pragma unroll
       for (int i = 0; i < kQF4; ++i)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sdata[i]), ro, full ? fvo[i] : tvo[i], soff,
-                                               0);
+                                               kPairStoreAux);
     };
     // Units k + 1 .. k + kAhead - 1 are in flight while unit k is skinned;
     // unit k + kAhead goes into unit k - 2's slot once that is stored.

@@ -23,13 +23,21 @@ step() {  # name timeout cmd...
   return $rc
 }
 PYT="python -u -m pytest -v --timeout 180 --timeout-method thread"
-for s in ${STEPS:-tests pairal path bench}; do
+for s in ${STEPS:-tests pairal path bench pmc stats}; do
   case $s in
     tests) step pytest_gpu 900 $PYT tests -m gpu || [ $? -eq 1 ] || exit 1 ;;
     pairal) MANO_TEST_LIB=libmano_hip_pairal.so step pytest_pairal 400 $PYT tests/test_gpu_parity.py \
               -k "standalone_lbs or phase_independent or other_mesh or fused_equals or library_is" || exit 1 ;;
-    path) step time_path 900 python tools/debug/time_path.py ${PATH_LIBS:-libmano_hip.so libmano_hip_pairal.so libmano_hip_restnt1.so libmano_hip_restnt2.so libmano_hip_restnt3.so libmano_hip_bpol0.so libmano_hip_bpol2.so} --reps 2 || exit 1 ;;
+    path) step time_path 900 python tools/debug/time_path.py ${PATH_LIBS:-libmano_hip.so libmano_hip_pairal.so libmano_hip_palnt1.so libmano_hip_palnt2.so libmano_hip_palnt3.so libmano_hip_pnt3.so libmano_hip_restnt1.so libmano_hip_restnt2.so libmano_hip_restnt3.so libmano_hip_bpol0.so libmano_hip_bpol2.so} --reps 2 || exit 1 ;;
     bench) step bench 400 python bench.py --steps 20 --warmup 5 || exit 1 ;;
+    pmc)  # blend_skin16 bytes per launch, verts-only and with rest_verts (align_bound.py --loop)
+      for lib in ${PMC_LIBS:-libmano_hip.so libmano_hip_legacy.so}; do
+        for what in verts rest; do
+          for c in WRITE_SIZE FETCH_SIZE; do
+            step pmc_${lib%.so}_${what}_$c 90 rocprofv3 --pmc $c -d $OUT/pmc_${lib%.so}_${what}_$c -o p --output-format csv -- python tools/debug/align_bound.py --loop $lib $what 20 || exit 1
+          done
+        done
+      done ;;
     stats) step kernel_stats 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o k --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu || exit 1 ;;
   esac
 done
