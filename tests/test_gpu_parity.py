@@ -483,7 +483,8 @@ def test_output_phase_independent(engine, dev, params, B, precision):
     variants (mano_layout.h) from the verts address: verts / rest_verts written
     at every 4-B phase of a 32-B sector (views offset by 0..7 floats) are
     bit-identical to the plain outputs, with and without translation, and to
-    the oracle."""
+    the oracle.  So are the unfused stages: the blend GEMM's v_posed (fp32)
+    and the standalone LBS reading and writing offset views."""
     engine.set_precision(precision)
     try:
         _phase_check(engine, dev, params, B)
@@ -507,15 +508,22 @@ def _phase_check(engine, dev, params, B):
             engine.stage_blend_skin(B, v, rest_verts=vp, trans=tr)
             v_only = torch.full((n + 8,), float("nan"), device=dev)[off:off + n].view(B, 778, 3)
             engine.stage_blend_skin(B, v_only, trans=tr)
-            # the unfused stages too (the blend GEMM's v_posed in the
-            # workspace, the standalone LBS into the offset view)
+            # the unfused stages too: the blend GEMM's v_posed into an offset
+            # view (fp32 only -- stage_blend is the fp32 GEMM in either
+            # precision, so its v_posed is the fp32 kernel's), and the
+            # standalone LBS from the offset rest_verts into an offset view
+            vp_blend = None
+            if engine.precision == "fp32":
+                vp_blend = torch.full((n + 8,), float("nan"), device=dev)[off:off + n].view(B, 778, 3)
+                engine.stage_blend(B, rest_verts=vp_blend)
             v_lbs = torch.full((n + 8,), float("nan"), device=dev)[off:off + n].view(B, 778, 3)
-            engine.stage_blend(B)
-            engine.stage_skin(B, v_lbs, trans=tr)
+            engine.stage_skin(B, v_lbs, rest_verts=vp, trans=tr)
             torch.cuda.synchronize()
             assert torch.equal(v, want["verts"]), (off, tr is None)
             assert torch.equal(vp, want["rest_verts"]), (off, tr is None)
             assert torch.equal(v_only, want["verts"]), (off, tr is None)
+            if vp_blend is not None:
+                assert torch.equal(vp_blend, want["rest_verts"]), (off, tr is None, "blend")
             assert torch.equal(v_lbs, want["verts"]), (off, tr is None, "unfused")
             assert torch.isnan(buf[:off]).all() and torch.isnan(buf[off + n:n + 32 + off]).all()
             assert torch.isnan(buf[2 * n + 32 + off:]).all()
