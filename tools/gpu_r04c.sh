@@ -26,6 +26,7 @@ PYT="python -u -m pytest -v --timeout 180 --timeout-method thread"
 for s in ${STEPS:-tests pairal path bench pmc stats}; do
   case $s in
     tests) step pytest_gpu 900 $PYT tests -m gpu || [ $? -eq 1 ] || exit 1 ;;
+    phase) step pytest_phase 300 $PYT tests/test_gpu_parity.py -k "phase_independent or library_is" || exit 1 ;;
     pairal) MANO_TEST_LIB=libmano_hip_pairal.so step pytest_pairal 400 $PYT tests/test_gpu_parity.py \
               -k "standalone_lbs or phase_independent or other_mesh or fused_equals or library_is" || exit 1 ;;
     path) step time_path 900 python tools/debug/time_path.py ${PATH_LIBS:-libmano_hip.so libmano_hip_pairal.so libmano_hip_palnt1.so libmano_hip_palnt2.so libmano_hip_palnt3.so libmano_hip_pnt3.so libmano_hip_restnt1.so libmano_hip_restnt2.so libmano_hip_restnt3.so libmano_hip_bpol0.so libmano_hip_bpol2.so} --reps 2 || exit 1 ;;
