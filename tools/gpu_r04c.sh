@@ -39,6 +39,10 @@ for s in ${STEPS:-tests pairal path bench pmc stats}; do
           done
         done
       done ;;
+    stamps)  # skin_pair per-wave cycle stamps, legacy vs aligned units
+      for lib in ${STAMP_LIBS:-libmano_hip_pstamp.so libmano_hip_palstamp.so}; do
+        step stamps_${lib%.so} 200 python tools/debug/pair_stamps.py $lib || exit 1
+      done ;;
     stats) step kernel_stats 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o k --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu || exit 1 ;;
   esac
 done
