@@ -364,10 +364,14 @@ __device__ __forceinline__ void bs_barrier() {
 #ifndef MANO_BS_NT_STORE
 #define MANO_BS_NT_STORE 1
 #endif
-// With rest_verts (diagnostic builds): bit 0 = verts nontemporal, bit 1 =
-// rest_verts nontemporal (round 3, with partial sectors: 0 was best).
+// With rest_verts: bit 0 = verts nontemporal, bit 1 = rest_verts
+// nontemporal.  Round 3, with partial sectors, 0 was best; with the
+// sector-aligned rows (round 4) 2 is: the rest_verts kernel 0.5555 / 0.5576
+// vs 0.5620 / 0.5667 ms, writes 1,313 vs 1,376 MB per launch (1.07x vs
+// 1.12x of 1,224), same digests; 1: no change, 3: 0.65 ms
+// (profiles/r04c_ab_path.jsonl, r04d_*).
 #ifndef MANO_BS_REST_NT
-#define MANO_BS_REST_NT 0
+#define MANO_BS_REST_NT 2
 #endif
 __device__ __forceinline__ float* byte_at(float* base, unsigned byte_off) {
   return reinterpret_cast<float*>(reinterpret_cast<char*>(base) + byte_off);
@@ -432,9 +436,8 @@ __global__ __launch_bounds__(256, MANO_BS_BLOCKS_PER_CU) void blend_skin16_kerne
   // (Diagnostic ablation builds store nothing or store elsewhere: no deferral,
   // so `pend` / `poff` are never flushed unassigned.)
   constexpr bool kDefer = kVposed && (MANO_BS_ABLATE == 0 || MANO_BS_ABLATE == 4);
-  // nontemporal only with one output stream (beside the rest_verts stream
-  // either one nontemporal took 0.71 vs 0.61 ms, both 0.86:
-  // profiles/r03m_ab_rest_nt.jsonl)
+  // the verts-only kernel's stores nontemporal; with rest_verts only the
+  // rest_verts stream (MANO_BS_REST_NT above)
   constexpr bool kVertsNt = kVposed ? bool(MANO_BS_REST_NT & 1) : bool(MANO_BS_NT_STORE);
   constexpr bool kRestNt = MANO_BS_REST_NT & 2;
   constexpr int kDeferAt = 2;
