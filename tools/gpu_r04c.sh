@@ -43,6 +43,12 @@ for s in ${STEPS:-tests pairal path bench pmc stats}; do
       for lib in ${STAMP_LIBS:-libmano_hip_pstamp.so libmano_hip_palstamp.so}; do
         step stamps_${lib%.so} 200 python tools/debug/pair_stamps.py $lib || exit 1
       done ;;
+    workloads)  # the other BASELINE configs on one GPU, the 1-rank nccl C4 line, the 2-rank gloo gather rehearsal
+      step bench_c5 300 python bench.py --workload C5 --steps 50 --warmup 5 --no-cpu --no-extra || exit 1
+      step bench_c3 300 python bench.py --workload C3 --steps 30 --warmup 3 --no-cpu --no-extra || exit 1
+      step bench_c4 300 python bench.py --workload C4 --steps 50 --warmup 5 --no-cpu --no-extra || exit 1
+      step bench_c4_pg 400 python bench.py --force-pg --workload C4 --steps 20 --warmup 5 --no-extra --no-dropin --cpu-seconds 5 || exit 1
+      step bench_c4_dp2 300 python bench.py --gpus 2 --backend gloo --workload C4 --batch 65536 --steps 10 --warmup 3 --no-cpu --no-extra || exit 1 ;;
     stats) step kernel_stats 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o k --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu || exit 1 ;;
   esac
 done
