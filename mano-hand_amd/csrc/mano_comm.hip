@@ -46,6 +46,19 @@ namespace {
 
 constexpr uint32_t kCommMagic = 0x434f4d4du;  // "COMM"
 
+// Shards are float rows, so they move as ncclFloat: a C4 shard of 5.0 GB is
+// 1.25e9 elements, inside a 32-bit count, where ncclChar would pass 5.0e9
+// (RCCL takes size_t counts, but nothing larger than 2^31 elements has run
+// here).  Both ends of a send / recv pair pick the type from the same byte
+// count, so they always agree.
+struct Elems {
+  ncclDataType_t type;
+  size_t count;
+};
+Elems elems(size_t bytes) {
+  return bytes % 4 == 0 ? Elems{ncclFloat, bytes / 4} : Elems{ncclChar, bytes};
+}
+
 int fail(int code, const char* fmt, ...) {
   char buf[512];
   va_list ap;
@@ -213,11 +226,14 @@ int mano_gather(mano_comm* c, const void* send, size_t send_bytes, void* recv,
   if (is_root) {
     for (int p = 0; p < c->n_ranks && res == ncclSuccess; ++p) {
       const size_t b = off[p + 1] - off[p];
-      if (p != root && b > 0)
-        res = r.recv(static_cast<char*>(recv) + off[p], b, ncclChar, p, c->comm, s);
+      if (p != root && b > 0) {
+        const Elems e = elems(b);
+        res = r.recv(static_cast<char*>(recv) + off[p], e.count, e.type, p, c->comm, s);
+      }
     }
   } else if (send_bytes > 0) {
-    res = r.send(send, send_bytes, ncclChar, root, c->comm, s);
+    const Elems e = elems(send_bytes);
+    res = r.send(send, e.count, e.type, root, c->comm, s);
   }
   const ncclResult_t end = r.group_end();
   if (res != ncclSuccess) return rccl_fail(r, res, is_root ? "ncclRecv" : "ncclSend");
@@ -237,8 +253,8 @@ int mano_allgather(mano_comm* c, const void* send, size_t send_bytes, void* recv
     return fail(MANO_EHIP, "hipSetDevice: %s", hipGetErrorString(guard.err));
   // RCCL's ring all-gather: each of the n - 1 steps forwards one shard to the
   // next rank, so every shard crosses n - 1 links in turn.
-  ncclResult_t res = r.all_gather(send, recv, send_bytes, ncclChar, c->comm,
-                                  static_cast<hipStream_t>(stream));
+  const Elems e = elems(send_bytes);
+  ncclResult_t res = r.all_gather(send, recv, e.count, e.type, c->comm, static_cast<hipStream_t>(stream));
   if (res != ncclSuccess) return rccl_fail(r, res, "ncclAllGather");
   return MANO_OK;
 }
