@@ -50,6 +50,10 @@ for s in ${STEPS:-tests pairal path bench pmc stats}; do
       step bench_c4_pg 400 python bench.py --force-pg --workload C4 --steps 20 --warmup 5 --no-extra --no-dropin --cpu-seconds 5 || exit 1
       step bench_c4_dp2 300 python bench.py --gpus 2 --backend gloo --workload C4 --batch 65536 --steps 10 --warmup 3 --no-cpu --no-extra || exit 1 ;;
     probe) step skin_align_probe 400 python tools/debug/skin_align_probe.py --reps 2 || exit 1 ;;
+    dist)  # the nccl 1-rank tests (after the ncclFloat change) and 8-rank gloo rehearsals sharing the GPU
+      step pytest_dist 400 $PYT tests/test_gpu_distributed.py || exit 1
+      step bench_c2_dp8 400 python bench.py --gpus 8 --backend gloo --steps 10 --warmup 3 --no-cpu --no-extra || exit 1
+      step bench_c4_dp8 400 python bench.py --gpus 8 --backend gloo --workload C4 --batch 16384 --steps 5 --warmup 2 --no-cpu --no-extra || exit 1 ;;
     stats) step kernel_stats 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o k --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu || exit 1 ;;
   esac
 done
