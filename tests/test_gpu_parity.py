@@ -407,7 +407,7 @@ def test_dropin_packed_io_matches_batched(engine, dev, params, graphs):
     assert np.array_equal(m.set_params(pose_abs=pose_a, shape=beta_a, trans=[0.01, 0.02, -0.03]), va_copy)
 
 
-@pytest.mark.parametrize("B", [1, 33, 200, 4096])
+@pytest.mark.parametrize("B", [1, 33, 200, 4096, 4099, 16387])
 def test_fused_equals_unfused(engine, dev, params, B):
     """blend_skin (fused, v_posed on chip) == blend then skin, bit for bit."""
     rng = np.random.default_rng(100 + B)
