@@ -54,6 +54,8 @@ for s in ${STEPS:-tests pairal path bench pmc stats}; do
       step pytest_dist 400 $PYT tests/test_gpu_distributed.py || exit 1
       step bench_c2_dp8 400 python bench.py --gpus 8 --backend gloo --steps 10 --warmup 3 --no-cpu --no-extra || exit 1
       step bench_c4_dp8 400 python bench.py --gpus 8 --backend gloo --workload C4 --batch 16384 --steps 5 --warmup 2 --no-cpu --no-extra || exit 1 ;;
+    clock) step clk 200 env TAG=${TAG:-r04c} LIBS=libmano_hip_stamp.so bash tools/debug/clk_stamps.sh || exit 1 ;;
+    fused) step pytest_fused 300 $PYT tests/test_gpu_parity.py -k "fused_equals_unfused" || exit 1 ;;
     stats) step kernel_stats 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o k --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu || exit 1 ;;
   esac
 done
