@@ -132,3 +132,31 @@ def check(rc: int) -> None:
 def last_error() -> str:
     msg = lib().mano_last_error()
     return msg.decode() if msg else ""
+
+
+class _PointerAttributes(ctypes.Structure):
+    """hipPointerAttribute_t (hip_runtime_api.h)."""
+    _fields_ = [("type", ctypes.c_int), ("device", ctypes.c_int), ("devicePointer", ctypes.c_void_p),
+                ("hostPointer", ctypes.c_void_p), ("isManaged", ctypes.c_int), ("allocationFlags", ctypes.c_uint)]
+
+
+_HIP_MEMORY_TYPE_HOST = 1
+
+
+def host_block_mapped(ptr: int) -> bool:
+    """True when `ptr` is pinned host memory that the HIP runtime maps into
+    the device address space at the same address (hipHostMalloc'd, e.g.
+    torch's pinned tensors), so kernels may read and write it directly."""
+    # the HIP runtime libmano_hip.so is linked against (dlsym on the
+    # library's handle searches its dependencies): never a second copy
+    try:
+        get_attrs = lib().hipPointerGetAttributes
+        get_last = lib().hipGetLastError
+    except AttributeError:
+        return False
+    a = _PointerAttributes()
+    rc = get_attrs(ctypes.byref(a), ctypes.c_void_p(ptr))
+    if rc != 0:
+        get_last()  # this query's error is not the caller's
+        return False
+    return a.type == _HIP_MEMORY_TYPE_HOST and a.devicePointer == ptr

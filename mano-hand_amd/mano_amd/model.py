@@ -456,6 +456,7 @@ class MANOModel:
         self.joints = None
         self._io = None
         self._graphs = {}
+        self._zc = {}
         self.update()
 
     def _dev(self, a) -> torch.Tensor:
@@ -494,11 +495,20 @@ class MANOModel:
         return self.verts.copy()
 
     # The batch-1 update's inputs and outputs, packed: one pinned host block
-    # and one device block each way, so a call is one H2D copy, the two
-    # forward kernels, one D2H copy and one stream sync -- captured once (per
-    # with/without translation) into a HIP graph and replayed, so a call
-    # costs one graph launch instead of four.
+    # each way.  Default (zero_copy): the two forward kernels read the input
+    # block and write the output block in host memory directly (pinned host
+    # memory is mapped into the device's address space), so a call is one
+    # mano_forward and one stream sync: 24.7 us for that part against 34.6 us
+    # for the copy form's graph replay (H2D, kernels, D2H) and 34.3 us for
+    # the same kernels launched from device buffers through ManoHip.forward
+    # (tools/debug/dropin_parts.py, profiles/r04i_dropin_parts.json; the
+    # kernels are the same, bit-identical results).  A block the runtime
+    # does not report as device-mapped takes the copy form: a device block
+    # each way, one H2D, the kernels, one D2H, captured once per translation
+    # mode and precision into a HIP graph (use_graphs) or launched eagerly.
     _IN = (("shape", (1, N_SHAPE)), ("pose", (1, N_JOINTS, 3)), ("trans", (1, 3)))
+    _OUT = ("verts", "joints", "rest_verts", "rest_joints", "rot_mats")
+    zero_copy = True
     use_graphs = True
 
     def _io_buffers(self):
@@ -544,12 +554,17 @@ class MANOModel:
         v_in["trans"][1][...] = self.trans
         with_trans = bool(np.any(self.trans))
         s = torch.cuda.current_stream(self.device)
-        # a graph replays the kernels of the precision it was captured with
-        g = self._graph((with_trans, self.engine.precision)) if self.use_graphs else None
-        if g is not None:
-            g.replay()
+        zc = self._zero_copy_args(with_trans) if self.zero_copy else None
+        if zc is not None:
+            # mano_forward on the pinned blocks (the handle's precision)
+            _abi.check(_abi.lib().mano_forward(*zc, ctypes.c_void_p(s.cuda_stream)))
         else:
-            self._update_body(with_trans)
+            # a graph replays the kernels of the precision it was captured with
+            g = self._graph((with_trans, self.engine.precision)) if self.use_graphs else None
+            if g is not None:
+                g.replay()
+            else:
+                self._update_body(with_trans)
         s.synchronize()
         host = {k: hv.astype(np.float64) for k, (_, hv) in v_out.items()}
         self.verts = host["verts"]
@@ -557,6 +572,24 @@ class MANOModel:
         self.J = host["rest_joints"]
         self.R = host["rot_mats"]
         self.joints = host["joints"]
+
+    def _zero_copy_args(self, with_trans):
+        """mano_forward's arguments (all but the stream) with the pinned host
+        blocks as its inputs and outputs, or None when either block is not
+        device-mapped host memory (then update() takes the copy form)."""
+        if with_trans not in self._zc:
+            d_in, h_in, v_in, d_out, h_out, v_out, ws = self._io_buffers()
+            args = None
+            if _abi.host_block_mapped(h_in.data_ptr()) and _abi.host_block_mapped(h_out.data_ptr()):
+                hp = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731  (numpy views of the blocks)
+                base = ws.data_ptr()
+                aligned = (base + 255) & ~255
+                args = (self.engine._h, 1, hp(v_in["shape"][1]), N_SHAPE, hp(v_in["pose"][1]),
+                        hp(v_in["trans"][1]) if with_trans else None,
+                        *(hp(v_out[k][1]) for k in self._OUT),
+                        ctypes.c_void_p(aligned), ctypes.c_size_t(ws.numel() - (aligned - base)))
+            self._zc[with_trans] = args
+        return self._zc[with_trans]
 
     def _update_body(self, with_trans):
         """H2D of the packed inputs, mano_forward, D2H of the packed outputs

@@ -127,3 +127,13 @@ def test_device_status_argument_checks():
     st = ctypes.c_int32(7)
     assert lib.mano_model_device_status(None, ctypes.byref(st), 0) == _abi.MANO_EINVAL
     assert st.value == 7
+
+
+def test_host_block_mapped_is_false_for_pageable_memory():
+    """The drop-in's zero-copy guard (hipPointerGetAttributes through the
+    runtime libmano_hip.so links) answers False for ordinary pageable host
+    memory -- here, with no GPU, for anything -- and never raises."""
+    import numpy as np
+    from mano_amd import _abi
+    a = np.zeros(64, dtype=np.float32)
+    assert _abi.host_block_mapped(a.ctypes.data) is False

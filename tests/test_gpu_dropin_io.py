@@ -83,14 +83,17 @@ def test_constructor_from_official_pickle(params, golden_steps, golden_batch, tm
     eng.close()
 
 
-def test_dropin_graph_workspace_is_private(params, golden_steps):
-    """The drop-in's captured HIP graph reads and writes its own batch-1
+@pytest.mark.parametrize("zero_copy", [True, False])
+def test_dropin_graph_workspace_is_private(params, golden_steps, zero_copy):
+    """The drop-in's batch-1 launches (on the pinned host blocks, or the
+    captured HIP graph of the copy form) read and write their own batch-1
     workspace: batched calls on the same engine over every pooled stream
     (torch.cuda.Stream() hands out a pool of handles), each growing that
-    stream's workspace, must not disturb the replays."""
+    stream's workspace, must not disturb them."""
     from mano_amd import MANOModel
     manifest, data = golden_steps
     m = MANOModel.from_params(params, device=0)
+    m.zero_copy = zero_copy
     assert m.use_graphs
     first = next(e for e in manifest if e["step"] > 0)
     kw = step_kwargs(first, data)

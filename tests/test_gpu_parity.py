@@ -362,15 +362,18 @@ def test_dropin_quirks(params):
     assert np.abs(m.joints - j0 - [0.1, -0.2, 0.3]).max() < 1e-6
 
 
-@pytest.mark.parametrize("graphs", [True, False])
-def test_dropin_packed_io_matches_batched(engine, dev, params, graphs):
-    """The drop-in's packed batch-1 I/O (one H2D, one D2H through pinned
-    buffers; replayed from a HIP graph or launched eagerly) returns the
-    batched engine's bits, and its results are owned copies: a later call
-    changes neither an earlier return nor its attributes."""
+@pytest.mark.parametrize("io", ["zero_copy", "graph", "eager"])
+def test_dropin_packed_io_matches_batched(engine, dev, params, io):
+    """The drop-in's packed batch-1 I/O (the kernels on the pinned host
+    blocks themselves; or one H2D, one D2H through them, replayed from a HIP
+    graph or launched eagerly) returns the batched engine's bits, and its
+    results are owned copies: a later call changes neither an earlier return
+    nor its attributes."""
     from mano_amd import MANOModel
     m = MANOModel.from_params(params, device=0)
-    m.use_graphs = graphs
+    m.zero_copy = io == "zero_copy"
+    m.use_graphs = io == "graph"
+    graphs = io == "graph"
     rng = np.random.default_rng(5)
     pose_a, pose_b = rng.normal(0, 0.5, (2, 16, 3))
     beta_a, beta_b = rng.normal(0, 1, (2, 10))
@@ -394,6 +397,9 @@ def test_dropin_packed_io_matches_batched(engine, dev, params, graphs):
     if graphs:  # both translation modes captured, and replayed (not the eager fallback)
         assert all(g[0] is not None for g in m._graphs.values())
         assert set(m._graphs) == {(True, "fp32"), (False, "fp32")}
+    if io == "zero_copy":  # both translation modes ran on the host blocks (not the copy form)
+        assert set(m._zc) == {True, False} and all(a is not None for a in m._zc.values())
+        assert not m._graphs
     # alternating modes and repeated inputs reproduce the same bits
     again = m.set_params(pose_abs=pose_a, shape=beta_a, trans=[0.01, 0.02, -0.03])
     assert np.array_equal(again, va_copy)
