@@ -56,7 +56,9 @@ for s in ${STEPS:-tests pairal path bench pmc stats}; do
       step bench_c4_dp8 400 python bench.py --gpus 8 --backend gloo --workload C4 --batch 16384 --steps 5 --warmup 2 --no-cpu --no-extra || exit 1 ;;
     clock) step clk 200 env TAG=${TAG:-r04c} LIBS=libmano_hip_stamp.so bash tools/debug/clk_stamps.sh || exit 1 ;;
     fused) step pytest_fused 300 $PYT tests/test_gpu_parity.py -k "fused_equals_unfused" || exit 1 ;;
-    dropin) step dropin_parts 200 python tools/debug/dropin_parts.py || exit 1 ;;
+    dropin) step pytest_dropin 300 $PYT tests/test_gpu_dropin_io.py tests/test_gpu_parity.py -k "dropin or stateful or export_obj" || exit 1
+      step dropin_parts 200 python tools/debug/dropin_parts.py || exit 1
+      step dropin_latency 200 python tools/debug/dropin_latency.py || exit 1 ;;
     stats) step kernel_stats 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o k --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu || exit 1 ;;
   esac
 done
