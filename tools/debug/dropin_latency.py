@@ -1,4 +1,5 @@
-"""Per-call latency of the drop-in MANOModel.set_params (batch 1): packed I/O
+"""Per-call latency of the drop-in MANOModel.set_params (batch 1): the kernels
+on the pinned host blocks (zero copy, the default), packed I/O through them
 (model.py: one pinned H2D, one D2H) replayed from a HIP graph, the same
 launched eagerly, and the round-2 form (a device tensor per input, a
 .double().cpu() per output); same model, same inputs, same process.
@@ -44,10 +45,12 @@ def main():
     shapes = rng.normal(0, 1, (a.calls, 10))
     res = {}
     packed = model_mod.MANOModel.update
-    for name, upd, graphs in (("graph", packed, True), ("packed", packed, False),
-                              ("per_array", per_array_update, False), ("graph_again", packed, True)):
+    for name, upd, graphs, zc in (("zero_copy", packed, True, True), ("graph", packed, True, False),
+                                  ("packed", packed, False, False), ("per_array", per_array_update, False, False),
+                                  ("zero_copy_again", packed, True, True)):
         model_mod.MANOModel.update = upd
         model_mod.MANOModel.use_graphs = graphs
+        model_mod.MANOModel.zero_copy = zc
         m = MANOModel.from_params(params, device=0)
         outs = []
         for i in range(30):
@@ -63,7 +66,8 @@ def main():
         m.engine.close()
     model_mod.MANOModel.update = packed
     model_mod.MANOModel.use_graphs = True
-    res["same_results"] = len({res[k]["digest"] for k in ("graph", "packed", "per_array")}) == 1
+    model_mod.MANOModel.zero_copy = True
+    res["same_results"] = len({res[k]["digest"] for k in ("zero_copy", "graph", "packed", "per_array")}) == 1
     print(json.dumps(res))
 
 
