@@ -210,6 +210,14 @@ int mano_free(int device, void* ptr);
 int mano_memcpy(int device, void* dst, const void* src, size_t bytes, int32_t kind,
                 void* stream);
 int mano_synchronize(int device);
+/* Pinned host memory mapped into every device's address space at the same
+ * address (hipHostMalloc): mano_forward and the stage calls may take it as
+ * their inputs and outputs directly -- the kernels read and write it over
+ * the host link, no copy -- which for a batch-1 call is faster than a copy
+ * each way (ABI 5).  Results are in host memory once the
+ * launch's stream (or mano_synchronize) has completed. */
+int mano_host_alloc(size_t bytes, void** out);
+int mano_host_free(void* ptr);
 
 /* ---- Synthetic workload (benchmarks, shard-invariance tests) ------------
  * Hand i of the batch is global hand first_index + i; its values are drawn
@@ -261,7 +269,7 @@ int mano_allgather(mano_comm* comm, const void* send, size_t send_bytes, void* r
 /* Message of the last failed call on this thread ("" if none). */
 const char* mano_last_error(void);
 
-/* ABI version, bumped on any signature change (4: + mano_allgather). */
+/* ABI version, bumped on any signature change (4: + mano_allgather; 5: + mano_host_alloc / mano_host_free). */
 int mano_abi_version(void);
 
 #ifdef __cplusplus

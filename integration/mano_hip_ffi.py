@@ -12,9 +12,13 @@ MI355X, keeping every attribute the reference sets there (`J` :83, `R` :86,
     model = MANOModel('dump_mano_left.pkl')
     verts = model.set_params(pose_pca=c, shape=beta, global_rot=[1, 0, 0])
 
-Device memory comes from the library itself (mano_alloc / mano_memcpy /
-mano_free), so the process never needs a GPU framework.  `Engine.forward`
-is the batched form: (B, 10) betas and (B, 16, 3) poses in one launch pair.
+Memory comes from the library itself, so the process never needs a GPU
+framework: by default the inputs and outputs live in one pinned host block
+(mano_host_alloc, mapped into the device's address space) that the kernels
+read and write directly -- a call is one mano_forward and one
+mano_synchronize, no copy; `Engine(..., zero_copy=False)` keeps them in
+device buffers (mano_alloc) moved by mano_memcpy.  `Engine.forward` is the
+batched form: (B, 10) betas and (B, 16, 3) poses in one launch pair.
 
 The library is found at $MANO_HIP_LIB, else at the build's in-tree path.
 """
@@ -42,6 +46,9 @@ for _name, _res, _args in (
         ("mano_alloc", ctypes.c_int, [ctypes.c_int, _sz, ctypes.POINTER(_p)]),
         ("mano_free", ctypes.c_int, [ctypes.c_int, _p]),
         ("mano_memcpy", ctypes.c_int, [ctypes.c_int, _p, _p, _sz, _i32, _p]),
+        ("mano_host_alloc", ctypes.c_int, [_sz, ctypes.POINTER(_p)]),
+        ("mano_host_free", ctypes.c_int, [_p]),
+        ("mano_synchronize", ctypes.c_int, [ctypes.c_int]),
         ("mano_last_error", ctypes.c_char_p, [])):
     _fn = getattr(_lib, _name)
     _fn.restype, _fn.argtypes = _res, _args
@@ -52,11 +59,18 @@ def _check(rc):
         raise RuntimeError(f"libmano_hip: {rc}: {_lib.mano_last_error().decode()}")
 
 
-class Engine:
-    """A device-resident MANO model plus device buffers for up to `capacity` hands."""
+_IO = (("betas", N_SHAPE), ("pose", N_JOINTS * 3), ("verts", None), ("joints", N_JOINTS * 3),
+       ("rest_verts", None), ("rest_joints", N_JOINTS * 3), ("rot_mats", N_JOINTS * 9))
 
-    def __init__(self, model, device=0, capacity=1):
+
+class Engine:
+    """A device-resident MANO model plus I/O buffers for up to `capacity` hands
+    (a pinned host block the kernels use directly, or device buffers)."""
+
+    def __init__(self, model, device=0, capacity=1, zero_copy=True):
         """model: anything with the reference's array attributes (mano_np.py:20-33)."""
+        self.zero_copy = zero_copy
+        self._host, self._views = None, {}
         f = lambda a: np.ascontiguousarray(np.asarray(a, dtype=np.float64))  # noqa: E731
         arrs = [f(model.mesh_template), f(model.mesh_shape_basis), f(model.mesh_pose_basis),
                 f(model.J_regressor), f(model.skinning_weights)]
@@ -77,28 +91,48 @@ class Engine:
         self._bufs[name] = ptr
 
     def _free_bufs(self):
-        for ptr in self._bufs.values():
-            _check(_lib.mano_free(self.device, ptr))
-        self._bufs = {}
+        for name, ptr in self._bufs.items():
+            if name == "workspace" or not self.zero_copy:
+                _check(_lib.mano_free(self.device, ptr))
+        self._bufs, self._views = {}, {}
+        if self._host is not None:
+            _check(_lib.mano_host_free(self._host))
+            self._host = None
 
     def _reserve(self, n):
         if n <= self.capacity:
             return
         self._free_bufs()
-        V = self.n_verts
-        for name, floats in (("betas", N_SHAPE), ("pose", N_JOINTS * 3), ("verts", V * 3),
-                             ("joints", N_JOINTS * 3), ("rest_verts", V * 3),
-                             ("rest_joints", N_JOINTS * 3), ("rot_mats", N_JOINTS * 9)):
-            self._alloc(name, 4 * floats * n)
+        sizes = [(name, n * (f if f is not None else 3 * self.n_verts)) for name, f in _IO]
+        if self.zero_copy:
+            # one pinned block, each array at a 256-B boundary
+            offs, o = {}, 0
+            for name, k in sizes:
+                offs[name] = o
+                o += (4 * k + 255) // 256 * 256
+            self._host = _p()
+            _check(_lib.mano_host_alloc(o, ctypes.byref(self._host)))
+            block = np.ctypeslib.as_array(ctypes.cast(self._host, ctypes.POINTER(ctypes.c_uint8)), shape=(o,))
+            for name, k in sizes:
+                self._views[name] = block[offs[name]:offs[name] + 4 * k].view(np.float32)
+                self._bufs[name] = _p(self._host.value + offs[name])
+        else:
+            for name, k in sizes:
+                self._alloc(name, 4 * k)
         self._ws_bytes = _lib.mano_forward_workspace_bytes(self._h, n)
         self._alloc("workspace", self._ws_bytes)
         self.capacity = n
 
     def _put(self, name, a):
         a = np.ascontiguousarray(a, dtype=np.float32)
-        _check(_lib.mano_memcpy(self.device, self._bufs[name], a.ctypes.data_as(_p), a.nbytes, H2D, None))
+        if self.zero_copy:
+            self._views[name][:a.size] = a.reshape(-1)
+        else:
+            _check(_lib.mano_memcpy(self.device, self._bufs[name], a.ctypes.data_as(_p), a.nbytes, H2D, None))
 
     def _get(self, name, shape):
+        if self.zero_copy:
+            return self._views[name][:int(np.prod(shape))].reshape(shape).astype(np.float64)
         out = np.empty(shape, dtype=np.float32)
         _check(_lib.mano_memcpy(self.device, out.ctypes.data_as(_p), self._bufs[name], out.nbytes, D2H, None))
         return out.astype(np.float64)
@@ -117,6 +151,8 @@ class Engine:
         _check(_lib.mano_forward(self._h, B, b["betas"], N_SHAPE, b["pose"], None, b["verts"],
                                  b["joints"], b["rest_verts"], b["rest_joints"], b["rot_mats"],
                                  b["workspace"], self._ws_bytes, None))
+        if self.zero_copy:  # the outputs are in the host block once the launches completed
+            _check(_lib.mano_synchronize(self.device))
         V = self.n_verts
         return {"verts": self._get("verts", (B, V, 3)), "J": self._get("rest_joints", (B, N_JOINTS, 3)),
                 "R": self._get("rot_mats", (B, N_JOINTS, 3, 3)),

@@ -94,7 +94,7 @@ int set_error(int code, const char* msg) {
 
 extern "C" {
 
-int mano_abi_version(void) { return 4; }
+int mano_abi_version(void) { return 5; }
 
 const char* mano_last_error(void) { return g_last_error.c_str(); }
 
@@ -478,6 +478,29 @@ int mano_free(int device, void* ptr) {
   if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
   hipError_t e = hipFree(ptr);
   if (e != hipSuccess) return hip_fail(e, "hipFree");
+  return MANO_OK;
+}
+
+int mano_host_alloc(size_t bytes, void** out) {
+  g_last_error.clear();
+  if (!out) return fail(MANO_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (bytes == 0) return MANO_OK;
+  // pinned, and mapped into every device's address space at the same
+  // address: kernels take it as operands directly
+  hipError_t e = hipHostMalloc(out, bytes, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    *out = nullptr;
+    return hip_fail(e, "hipHostMalloc");
+  }
+  return MANO_OK;
+}
+
+int mano_host_free(void* ptr) {
+  g_last_error.clear();
+  if (!ptr) return MANO_OK;
+  hipError_t e = hipHostFree(ptr);
+  if (e != hipSuccess) return hip_fail(e, "hipHostFree");
   return MANO_OK;
 }
 

@@ -79,6 +79,8 @@ SIGNATURES = {
     "mano_rodrigues": (ctypes.c_int, [ctypes.c_int, _i64, _p, _p, _p]),
     "mano_alloc": (ctypes.c_int, [ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(_p)]),
     "mano_free": (ctypes.c_int, [ctypes.c_int, _p]),
+    "mano_host_alloc": (ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(_p)]),
+    "mano_host_free": (ctypes.c_int, [_p]),
     "mano_memcpy": (ctypes.c_int, [ctypes.c_int, _p, _p, ctypes.c_size_t, _i32, _p]),
     "mano_synchronize": (ctypes.c_int, [ctypes.c_int]),
     "mano_synthetic_inputs": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, _i64, _i64, ctypes.c_float,

@@ -17,7 +17,7 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, n), n
         assert n in _abi.SIGNATURES, f"{n} declared in the header but not bound"
     assert set(_abi.SIGNATURES) == set(names)
-    assert lib.mano_abi_version() == 4
+    assert lib.mano_abi_version() == 5
 
 
 @pytest.mark.parametrize("cc,lang", [("g++", "c++"), ("gcc", "c")])
@@ -137,3 +137,12 @@ def test_host_block_mapped_is_false_for_pageable_memory():
     from mano_amd import _abi
     a = np.zeros(64, dtype=np.float32)
     assert _abi.host_block_mapped(a.ctypes.data) is False
+
+
+def test_host_alloc_argument_checks():
+    """ABI 5's pinned host allocation: argument checks without a GPU."""
+    lib = _abi.lib()
+    p = ctypes.c_void_p(1)
+    assert lib.mano_host_alloc(0, ctypes.byref(p)) == _abi.MANO_OK and not p.value
+    assert lib.mano_host_alloc(16, None) == _abi.MANO_EINVAL
+    assert lib.mano_host_free(None) == _abi.MANO_OK

@@ -1,8 +1,9 @@
 """The maintainer's binding (integration/mano_hip_ffi.py): numpy + ctypes only.
 
 A child process that never imports torch drives libmano_hip.so through the
-C-ABI alone (mano_alloc / mano_memcpy / mano_forward / mano_free): the golden
-batch through `Engine.forward`, and the reference's stateful set_params
+C-ABI alone (mano_host_alloc / mano_alloc / mano_forward / mano_synchronize,
+and the copy form's mano_memcpy): the golden batch through `Engine.forward`
+in both I/O forms (bit-identical), and the reference's stateful set_params
 script with `update` patched onto a stand-in of the reference class (the
 oracle's restatement of mano_np.py:35-77, its arrays bound under the
 reference's attribute names), each within 1e-5 m of the reference goldens.
@@ -33,6 +34,12 @@ for k_got, k_ref in (("verts", "verts"), ("J", "J"), ("R", "R"), ("rest_verts", 
     err = np.abs(out[k_got] - g[k_ref]).max()
     assert err <= 1e-5, (k_got, err)
 eng.close()
+# the copy form (device buffers + mano_memcpy) gives the zero-copy form's bits
+eng_c = mano_hip_ffi.Engine(type("M", (), params), device=0, capacity=24, zero_copy=False)
+out_c = eng_c.forward(g["betas"], g["pose"])
+for k in out:
+    assert np.array_equal(out[k], out_c[k]), k
+eng_c.close()
 
 class Ref(StatefulOracle):
     """Stand-in for mano_np.MANOModel: the reference's attributes + set_params."""

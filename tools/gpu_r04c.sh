@@ -59,6 +59,8 @@ for s in ${STEPS:-tests pairal path bench pmc stats}; do
     dropin) step pytest_dropin 300 $PYT tests/test_gpu_dropin_io.py tests/test_gpu_parity.py -k "dropin or stateful or export_obj" || exit 1
       step dropin_parts 200 python tools/debug/dropin_parts.py || exit 1
       step dropin_latency 200 python tools/debug/dropin_latency.py || exit 1 ;;
+    ffi) step pytest_ffi 300 $PYT tests/test_gpu_ffi.py tests/test_abi.py || exit 1
+      step ffi_latency 200 python tools/debug/ffi_latency.py || exit 1 ;;
     stats) step kernel_stats 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o k --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu || exit 1 ;;
   esac
 done
