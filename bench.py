@@ -215,8 +215,10 @@ def cpu_baseline(procs, seconds):
 
 def dropin_latency(params, device, calls=300, warmup=30, seed=7):
     """The drop-in's batch-1 call (MANOModel.set_params(pose_abs, shape): host
-    float64 in, H2D, the two forward kernels, D2H, float64 attributes out) --
-    config C1's operation on the GPU, timed per call on the host clock."""
+    float64 in, the two forward kernels on the pinned host blocks (or, when
+    they are not device-mapped, H2D + kernels + D2H), float64 attributes
+    out) -- config C1's operation on the GPU, timed per call on the host
+    clock."""
     from mano_amd import MANOModel
     m = MANOModel.from_params(params, device=device)
     rng = np.random.default_rng(seed)
@@ -233,6 +235,7 @@ def dropin_latency(params, device, calls=300, warmup=30, seed=7):
     ts = np.sort(np.asarray(ts)) * 1e6
     return {"op": "MANOModel.set_params(pose_abs=(16,3), shape=(10,)) -> verts (778,3) float64, "
                   "with J, R, rest_verts, joints updated (mano_np.py:48-115)",
+            "io": "zero_copy" if m._zc.get(False) is not None else ("graph" if m.use_graphs else "eager"),
             "us_per_call_median": float(np.median(ts)), "us_per_call_p90": float(ts[int(0.9 * len(ts))]),
             "us_per_call_mean": float(ts.mean()), "calls": calls}
 
