@@ -653,17 +653,19 @@ def main(argv=None):
             if path != args.path:
                 time_path(path, ms)
         # The standalone LBS back to back (each launch after another LBS
-        # launch, as rocprof's kernel average sees it); in the unfused path
-        # it follows the blend GEMM's 612 MB of freshly written v_posed.
-        for _ in range(20):
+        # launch, as rocprof's kernel trace sees it); in the unfused path it
+        # follows the blend GEMM's 612 MB of freshly written v_posed.  One
+        # event pair around 50 launches (a timing event between launches
+        # adds its own few microseconds to each; §4, "Timing events cost").
+        for _ in range(50):
             model.stage_skin(B, scratch[0], trans=trans)
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(50)]
-        for e0, e1 in evs:
-            e0.record(stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(50):
             model.stage_skin(B, scratch[0], trans=trans)
-            e1.record(stream)
+        e1.record(stream)
         torch.cuda.synchronize()
-        ms["skin_back_to_back"] = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+        ms["skin_back_to_back"] = e0.elapsed_time(e1) / 50
         model.set_precision(other)
         for path in ("forward", "unfused"):
             time_path(path, ms_other)
@@ -749,7 +751,8 @@ def main(argv=None):
         if "skin_back_to_back" in ms:
             b2b = ms["skin_back_to_back"]
             kernels["skin"].update({"ms_back_to_back": b2b, "achieved_GBs_back_to_back": gbs(SKIN_BYTES_PER_HAND, b2b),
-                                    "frac_back_to_back": gbs(SKIN_BYTES_PER_HAND, b2b) / PEAK_HBM_GBS})
+                                    "frac_back_to_back": gbs(SKIN_BYTES_PER_HAND, b2b) / PEAK_HBM_GBS,
+                                    "timing_back_to_back": "one HIP event pair around 50 launches after 50 warm ones"})
     for k, v in kernels.items():
         v["in_timed_path"] = k in in_path
         v["precision"] = args.precision
