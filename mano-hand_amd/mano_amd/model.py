@@ -530,6 +530,14 @@ class MANOModel:
 
             d_in, h_in, v_in = carve(self._IN, self.device, True)
             d_out, h_out, v_out = carve(outs, self.device, True)
+            # the outputs' places in the host block (one float64 conversion per call)
+            o = 0
+            layout = []
+            for name, shp in outs:
+                k = int(np.prod(shp))
+                layout.append((name, o, o + k, shp[1:]))
+                o += k
+            self._out_layout = tuple(layout)
             # the batch-1 forward's own workspace: the eager calls and every
             # captured graph use it (a graph holds its raw pointer), and it is
             # never one of the engine's per-stream workspaces, which another
@@ -552,7 +560,8 @@ class MANOModel:
         v_in["shape"][1][...] = shape
         v_in["pose"][1][...] = pose.reshape(self.n_joints, 3)
         v_in["trans"][1][...] = self.trans
-        with_trans = bool(np.any(self.trans))
+        t = self.trans  # (3,) float64; three scalar tests cost less than np.any here
+        with_trans = bool(t[0] != 0 or t[1] != 0 or t[2] != 0)
         s = torch.cuda.current_stream(self.device)
         zc = self._zero_copy_args(with_trans) if self.zero_copy else None
         if zc is not None:
@@ -566,7 +575,8 @@ class MANOModel:
             else:
                 self._update_body(with_trans)
         s.synchronize()
-        host = {k: hv.astype(np.float64) for k, (_, hv) in v_out.items()}
+        blk = h_out.numpy().astype(np.float64)  # float64 views of one conversion
+        host = {k: blk[a:b].reshape(shp) for k, a, b, shp in self._out_layout}
         self.verts = host["verts"]
         self.rest_verts = host["rest_verts"]
         self.J = host["rest_joints"]
