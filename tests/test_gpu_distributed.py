@@ -166,3 +166,38 @@ def test_bench_one_rank_nccl_process_group(impl):
         assert line["cpu_baseline"]["value"] > 0
         assert line["roofline"]["traffic"] > 0
         assert line["roofline"]["traffic_source"].startswith("measured in this run")
+
+
+def _visible_gpus():
+    # counting devices does not initialise the GPU in this process
+    return torch.cuda.device_count()
+
+
+@pytest.mark.skipif(_visible_gpus() < 2, reason="the RCCL gather across ranks needs 2 GPUs (RCCL refuses two ranks on one)")
+@pytest.mark.parametrize("impl", ["sendrecv", "allgather"])
+def test_bench_two_gpus_nccl_gather(impl):
+    """On a node with 2+ GPUs: bench.py --gpus 2 on the nccl backend with the
+    C4 gather -- mano_gather's grouped ncclSend / ncclRecv (or RCCL's ring
+    all-gather) between two ranks for real, GPU 0's assembled verts / joints
+    checked bit for bit against hands regenerated by global index over both
+    ranks' ranges, both ranks' sampled hands against the oracle, and the
+    gather's bytes and link figures in the line."""
+    import json
+    import subprocess
+    B = 16384
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "nccl",
+           "--workload", "C4", "--batch", str(B), "--steps", "5", "--warmup", "2", "--ramp-seconds", "0",
+           "--gather-impl", impl, "--no-extra", "--no-dropin", "--no-cpu", "--no-live-pmc"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["process_group"]["backend"] == "nccl"
+    assert line["gather_check"]["bit_exact"] and line["gather_check"]["ranks"] == 2, line["gather_check"]
+    assert line["correctness"]["pass"] and line["correctness"]["ranks_checked"] == 2, line["correctness"]
+    g = line["gather"]
+    assert g["impl"] == impl and g["ms"] > 0
+    assert g["bytes_to_gpu0"] == B * (778 * 3 + 16 * 3) * 4
+    assert g["GBs_to_gpu0"] > 0 and g["link_frac"] is not None
+    c = g["compare"]
+    assert c["bit_exact"] and c["ms"] > 0
