@@ -168,6 +168,37 @@ def test_bench_one_rank_nccl_process_group(impl):
         assert line["roofline"]["traffic_source"].startswith("measured in this run")
 
 
+def _nccl_worker(rank, world, port, q):
+    """Rank `rank` on GPU `rank`: its ragged shard of N_TOTAL hands, gathered
+    to rank 0 through the C-ABI's RCCL gather (AbiGather -> mano_gather)."""
+    for p in (os.path.join(REPO, "mano-hand_amd"), REPO):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+    from mano_amd import ManoHip, synthetic_params
+    from mano_amd.distributed import AbiGather, shard_range
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(rank)
+    dev = torch.device("cuda", rank)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    try:
+        a, b = shard_range(N_TOTAL, rank, world)
+        betas, pose, trans = _inputs()
+        m = ManoHip(synthetic_params(0), device=rank)
+        f = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)  # noqa: E731
+        out = m.forward(f(betas[a:b]), f(pose[a:b]), f(trans[a:b]), joints=True)
+        g = AbiGather(rank)
+        fv = g.gather(out["verts"], N_TOTAL, root=0)
+        fj = g.gather(out["joints"], N_TOTAL, root=0)
+        torch.cuda.synchronize()
+        q.put((rank, None if fv is None else (fv.cpu().numpy(), fj.cpu().numpy())))
+        dist.barrier()
+        m.close()
+    finally:
+        dist.destroy_process_group()
+
+
 def _visible_gpus():
     # counting devices does not initialise the GPU in this process
     return torch.cuda.device_count()
@@ -201,3 +232,30 @@ def test_bench_two_gpus_nccl_gather(impl):
     assert g["GBs_to_gpu0"] > 0 and g["link_frac"] is not None
     c = g["compare"]
     assert c["bit_exact"] and c["ms"] > 0
+
+
+@pytest.mark.skipif(_visible_gpus() < 2, reason="the RCCL gather across ranks needs 2 GPUs")
+def test_abi_gather_ragged_two_gpus():
+    """mano_gather between two GPUs with ragged shards (1,003 hands: 502 +
+    501): GPU 0's assembled verts / joints equal the single-process forward
+    of the whole batch bit for bit."""
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_nccl_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=200) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[1] is None
+    verts, joints = got[0]
+    ref_v, ref_j = _forward(*_inputs())
+    assert np.array_equal(verts, ref_v.numpy())
+    assert np.array_equal(joints, ref_j.numpy())
