@@ -123,6 +123,9 @@ def parse(argv=None):
     ap.add_argument("--gather-compare-reps", type=int, default=4,
                     help="after timing, run the other gather form this many times and report it "
                          "beside the timed one (0 = skip; RCCL only)")
+    ap.add_argument("--watchdog-seconds", type=float, default=900.0,
+                    help="with a process group: a rank still running after this many seconds dumps "
+                         "its Python stacks and exits (a hang becomes a diagnosed failure; 0 = off)")
     return ap.parse_args(argv)
 
 
@@ -454,6 +457,12 @@ def main(argv=None):
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.watchdog_seconds > 0 and (world > 1 or args.force_pg):
+        # A rank stuck in a collective (RCCL init, the gather, a barrier)
+        # prints every thread's Python stack and exits, so a first multi-GPU
+        # run that hangs leaves a diagnosis instead of a silent timeout.
+        import faulthandler
+        faulthandler.dump_traceback_later(args.watchdog_seconds, exit=True)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and args.gpus not in (1, world):
