@@ -575,7 +575,11 @@ def main(argv=None):
             if gmarks is not None:
                 gmarks[1].record(stream)
 
-    # Clock ramp, then the untimed warmup.
+    # Clock ramp, then the untimed warmup.  With a process group the ranks
+    # agree on when the ramp ends (one small all_reduce per 10 steps): with
+    # the C4 gather every step is a collective, and ranks that each read
+    # their own clock could run different numbers of ramp steps -- the
+    # unmatched gathers would hang.
     t_ramp = time.perf_counter()
     n_ramp = 0
     while True:
@@ -583,7 +587,13 @@ def main(argv=None):
             step()
         n_ramp += 10
         torch.cuda.synchronize()
-        if time.perf_counter() - t_ramp >= args.ramp_seconds:
+        done = time.perf_counter() - t_ramp >= args.ramp_seconds
+        if dist_on:
+            flag = torch.tensor([1 if done else 0], device=dev if args.backend == "nccl" else "cpu",
+                                dtype=torch.int32)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+            done = bool(flag.item())
+        if done:
             break
     t_ramp = time.perf_counter() - t_ramp
     for _ in range(args.warmup):

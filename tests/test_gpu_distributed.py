@@ -259,3 +259,22 @@ def test_abi_gather_ragged_two_gpus():
     ref_v, ref_j = _forward(*_inputs())
     assert np.array_equal(verts, ref_v.numpy())
     assert np.array_equal(joints, ref_j.numpy())
+
+
+def test_bench_c4_ramp_ends_together():
+    """With the C4 gather every step is a collective, so the ranks must run
+    the same number of clock-ramp steps: a 1-s ramp of short steps (many
+    10-step chunks, each rank reading its own clock) completes on 2 gloo
+    ranks, and both ranks report the same ramp step count."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                        "--workload", "C4", "--batch", "256", "--steps", "5", "--warmup", "2",
+                        "--ramp-seconds", "1", "--no-cpu", "--no-extra", "--no-dropin", "--no-live-pmc",
+                        "--watchdog-seconds", "200"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["ramp"]["steps"] > 10, line["ramp"]
+    assert line["gather_check"]["bit_exact"]
