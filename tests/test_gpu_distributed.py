@@ -265,7 +265,8 @@ def test_bench_c4_ramp_ends_together():
     """With the C4 gather every step is a collective, so the ranks must run
     the same number of clock-ramp steps: a 1-s ramp of short steps (many
     10-step chunks, each rank reading its own clock) completes on 2 gloo
-    ranks, and both ranks report the same ramp step count."""
+    ranks with GPU 0's gathered rows intact (ranks that disagreed would
+    leave a gather unmatched: a hang, ended by the 200-s watchdog)."""
     import json
     import subprocess
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
