@@ -56,6 +56,12 @@ BLEND_FLOP_PER_HAND = 2 * NCOL * K                 # 676,860
 SKIN_BYTES_PER_HAND = NCOL * 4 * 2 + 16 * 12 * 4   # v_posed in + verts out + transforms = 19,440
 LBS_T_FLOP_PER_HAND = V * 16 * 12 * 2              # the transform blend (on MFMA when fused) = 298,752
 FUSED_MFMA_FLOP_PER_HAND = BLEND_FLOP_PER_HAND + LBS_T_FLOP_PER_HAND  # 975,612
+# SURVEY.md §8(d)'s per-hand figure for the fused kernel, the roofline's
+# numerator: GEMM 676,860 + LBS 778 x 405 = 315,090 (the transform blend's
+# 384 flop per vertex plus the apply's 21, which run on the VALU -- the same
+# fp32 datapath and peak as the MFMAs on gfx950).
+LBS_FLOP_PER_HAND = V * 405                        # 315,090
+FUSED_FLOP_PER_HAND = BLEND_FLOP_PER_HAND + LBS_FLOP_PER_HAND  # 991,950
 FUSED_BYTES_PER_HAND = 160 * 4 + 16 * 12 * 4 + NCOL * 4     # X row + transforms in, verts out = 10,744
 ARTICULATE_BYTES_PER_HAND = (10 + 48) * 4 + 16 * 12 * 4 + 16 * 3 * 4 + 160 * 4  # in + A + joints + X row = 1,832
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, spec
@@ -744,11 +750,14 @@ def main(argv=None):
                                  "bound": "latency", "achieved_GBs": a,
                                  "bytes_per_hand": ARTICULATE_BYTES_PER_HAND}
     if "blend_skin" in ms and args.precision == "fp32":
-        a = tflops(FUSED_MFMA_FLOP_PER_HAND, ms["blend_skin"])
+        a = tflops(FUSED_FLOP_PER_HAND, ms["blend_skin"])
+        a_mfma = tflops(FUSED_MFMA_FLOP_PER_HAND, ms["blend_skin"])
         kernels["blend_skin"] = {"kernel": "blend_skin16_kernel", "ms": ms["blend_skin"],
                                  "bound": "mfma", "achieved_TFLOPs": a,
                                  "frac": a / PEAK_FP32_TFLOPS,
-                                 "flop_per_hand": FUSED_MFMA_FLOP_PER_HAND,
+                                 "flop_per_hand": FUSED_FLOP_PER_HAND,
+                                 "mfma_only": {"flop_per_hand": FUSED_MFMA_FLOP_PER_HAND, "achieved_TFLOPs": a_mfma,
+                                               "frac": a_mfma / PEAK_FP32_TFLOPS},
                                  "blend_gemm_TFLOPs": tflops(BLEND_FLOP_PER_HAND, ms["blend_skin"])}
     elif "blend_skin" in ms:  # f16x3: the split GEMM runs at 16/3 x the fp32 rate; HBM stores bound it
         a = gbs(FUSED_BYTES_PER_HAND, ms["blend_skin"])
@@ -810,6 +819,8 @@ def main(argv=None):
             roof = {"kernel": kd["kernel"], "bound": "hbm", "achieved": kd["achieved_GBs"],
                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": kd["frac"]}
         roof["algorithmic_per_hand"] = kd.get("flop_per_hand", kd.get("bytes_per_hand"))
+        if "mfma_only" in kd:  # the same launches counted with the MFMA flops alone (rounds 1-3's numerator)
+            roof["mfma_only"] = kd["mfma_only"]
         roof["hands_per_launch"] = B
         roof["timed_in_region"] = dominant in in_path
 

@@ -51,6 +51,8 @@ def test_workloads_match_baseline_configs():
 def test_algorithmic_work_constants():
     assert bench.BLEND_FLOP_PER_HAND == 676860
     assert bench.FUSED_MFMA_FLOP_PER_HAND == 975612
+    # GEMM 676,860 + LBS 778 x 405 = 315,090 (the roofline's numerator)
+    assert bench.LBS_FLOP_PER_HAND == 315090 and bench.FUSED_FLOP_PER_HAND == 991950
     assert bench.SKIN_BYTES_PER_HAND == 19440
     assert bench.FUSED_BYTES_PER_HAND == 10744
 
