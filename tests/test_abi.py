@@ -146,3 +146,27 @@ def test_host_alloc_argument_checks():
     assert lib.mano_host_alloc(0, ctypes.byref(p)) == _abi.MANO_OK and not p.value
     assert lib.mano_host_alloc(16, None) == _abi.MANO_EINVAL
     assert lib.mano_host_free(None) == _abi.MANO_OK
+
+
+def test_ffi_binding_signatures_match_header():
+    """integration/mano_hip_ffi.py (the torch-free binding) declares every C
+    function it calls with the header's parameter count, and imports without
+    torch and without a GPU (loading the library runs nothing)."""
+    import re
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); import mano_hip_ffi as f; "
+            "print({n: len(getattr(f._lib, n).argtypes) for n in ('mano_model_create', 'mano_forward', "
+            "'mano_alloc', 'mano_free', 'mano_memcpy', 'mano_host_alloc', 'mano_host_free', 'mano_synchronize', "
+            "'mano_forward_workspace_bytes', 'mano_model_destroy')}); print('torch' in sys.modules)"
+            % os.path.join(REPO, "integration"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    counts, torch_loaded = r.stdout.strip().splitlines()
+    assert torch_loaded == "False"
+    header = open(os.path.join(REPO, "include", "mano_hip.h")).read()
+    for name, n in eval(counts).items():
+        m = re.search(r"\b%s\(([^)]*)\)" % name, header)
+        assert m, name
+        params = [p for p in m.group(1).split(",") if p.strip() and p.strip() != "void"]
+        assert len(params) == n, (name, len(params), n)
