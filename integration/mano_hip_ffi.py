@@ -61,6 +61,7 @@ def _check(rc):
 
 _IO = (("betas", N_SHAPE), ("pose", N_JOINTS * 3), ("verts", None), ("joints", N_JOINTS * 3),
        ("rest_verts", None), ("rest_joints", N_JOINTS * 3), ("rot_mats", N_JOINTS * 9))
+_OUTS = ("verts", "joints", "rest_verts", "rest_joints", "rot_mats")
 
 
 class Engine:
@@ -105,7 +106,8 @@ class Engine:
         self._free_bufs()
         sizes = [(name, n * (f if f is not None else 3 * self.n_verts)) for name, f in _IO]
         if self.zero_copy:
-            # one pinned block, each array at a 256-B boundary
+            # one pinned block, each array at a 256-B boundary; the outputs
+            # follow the inputs, so one float64 conversion reads them all
             offs, o = {}, 0
             for name, k in sizes:
                 offs[name] = o
@@ -116,6 +118,8 @@ class Engine:
             for name, k in sizes:
                 self._views[name] = block[offs[name]:offs[name] + 4 * k].view(np.float32)
                 self._bufs[name] = _p(self._host.value + offs[name])
+            self._out_block = block[offs["verts"]:].view(np.float32)
+            self._out_at = {name: (offs[name] - offs["verts"]) // 4 for name, _ in sizes if name in _OUTS}
         else:
             for name, k in sizes:
                 self._alloc(name, 4 * k)
@@ -151,9 +155,15 @@ class Engine:
         _check(_lib.mano_forward(self._h, B, b["betas"], N_SHAPE, b["pose"], None, b["verts"],
                                  b["joints"], b["rest_verts"], b["rest_joints"], b["rot_mats"],
                                  b["workspace"], self._ws_bytes, None))
+        V = self.n_verts
         if self.zero_copy:  # the outputs are in the host block once the launches completed
             _check(_lib.mano_synchronize(self.device))
-        V = self.n_verts
+            out = self._out_block.astype(np.float64)  # one conversion, then views of it
+            at = self._out_at
+            view = lambda name, shape: out[at[name]:at[name] + int(np.prod(shape))].reshape(shape)  # noqa: E731
+            return {"verts": view("verts", (B, V, 3)), "J": view("rest_joints", (B, N_JOINTS, 3)),
+                    "R": view("rot_mats", (B, N_JOINTS, 3, 3)), "rest_verts": view("rest_verts", (B, V, 3)),
+                    "joints": view("joints", (B, N_JOINTS, 3))}
         return {"verts": self._get("verts", (B, V, 3)), "J": self._get("rest_joints", (B, N_JOINTS, 3)),
                 "R": self._get("rot_mats", (B, N_JOINTS, 3, 3)),
                 "rest_verts": self._get("rest_verts", (B, V, 3)),
