@@ -30,20 +30,35 @@ does not leave the timed steps on the ramp.
 
 Rank 0 prints ONE JSON line with the whole-node hands/s, the roofline of the
 dominant kernel (per-kernel durations from HIP events recorded on the launch
-stream around every 8th timed step; at N = 1 its HBM bytes per launch measured
-in the same run by two rocprofv3 --pmc passes, FETCH_SIZE and WRITE_SIZE, over a
-short child run of this bench after the timed region) and, at N = 1, the CPU
-baseline: the float64 restatement of mano_np.py (oracle/, "port") timed on this
-host's cores.
+stream around every E-th timed step, E = min(--event-every, steps // 5): every
+4th at the driver's 20 steps; its HBM bytes per launch measured in the same run
+by two rocprofv3 --pmc passes, FETCH_SIZE and WRITE_SIZE, over a short child
+run of this bench on rank 0's GPU after the timed region) and the CPU baseline:
+the float64 restatement of mano_np.py (oracle/, "port") timed on this host's
+cores by rank 0 at every N (the other ranks wait with idle GPUs).
+
+Failure handling with a process group (every N > 1 run): a collective that
+stalls raises after --pg-timeout-seconds (240); a rank still inside the
+collective phases after --watchdog-seconds (420, from process start) prints a
+`"status": "watchdog"` JSON line naming its phase (rank 0 on stdout) and every
+thread's Python stack, then exits; a rank that torchrun terminates dumps its
+stacks too (SIGTERM).  Rank 0's host legs (PMC passes, drop-in, CPU baseline)
+are fitted into --deadline-seconds (540, from process start; the driver's
+bench lease is 600 s), a leg that no longer fits is skipped and says so.
 """
 import argparse
+import datetime
+import faulthandler
 import json
 import os
+import signal
 import socket
 import subprocess
 import sys
+import threading
 import time
 
+T_START = time.monotonic()   # process start: the watchdog and the deadline count from here
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "mano-hand_amd"))
 sys.path.insert(0, REPO)
@@ -129,10 +144,111 @@ def parse(argv=None):
     ap.add_argument("--gather-compare-reps", type=int, default=4,
                     help="after timing, run the other gather form this many times and report it "
                          "beside the timed one (0 = skip; RCCL only)")
-    ap.add_argument("--watchdog-seconds", type=float, default=900.0,
-                    help="with a process group: a rank still running after this many seconds dumps "
-                         "its Python stacks and exits (a hang becomes a diagnosed failure; 0 = off)")
+    ap.add_argument("--watchdog-seconds", type=float, default=420.0,
+                    help="with a process group: a rank still in the collective phases this many "
+                         "seconds after process start prints a status line and its Python stacks and "
+                         "exits (a hang becomes a diagnosed failure inside the driver's 600-s lease; 0 = off)")
+    ap.add_argument("--pg-timeout-seconds", type=float, default=240.0,
+                    help="init_process_group timeout: a collective that stalls this long raises")
+    ap.add_argument("--deadline-seconds", type=float, default=540.0,
+                    help="wall-time budget from process start: rank 0's host legs (PMC passes, "
+                         "drop-in, CPU baseline) are shortened or skipped to end inside it")
+    ap.add_argument("--inject-hang", type=int, default=None,
+                    help="(tests, with --launch-check) this rank skips the collective and stalls")
     return ap.parse_args(argv)
+
+
+METRIC = "posed hand meshes/sec (whole node)"
+WATCHDOG_EXIT = 3
+
+
+def status_line(status, phase, rank, world, **extra):
+    """The JSON line of a run that did not finish (watchdog / error): the
+    metric with value null, the phase it was in and how long it had run."""
+    line = {"metric": METRIC, "value": None, "unit": "hands/s", "n_gpus": world, "status": status,
+            "phase": phase, "rank": rank, "elapsed_s": round(time.monotonic() - T_START, 3)}
+    line.update(extra)
+    return line
+
+
+class Watchdog:
+    """Per-rank guard of the collective phases of a process-group run.
+
+    `enter(phase)` names what the rank is doing; once armed, a rank still
+    running at the deadline prints `status_line("watchdog", phase)` (rank 0 on
+    stdout, the others on stderr) and every thread's Python stack, then exits
+    with WATCHDOG_EXIT -- so a first multi-GPU run that hangs ends as a
+    diagnosed failure before the driver's lease kills it.  The check runs on
+    a Python thread (every blocking call of the run -- torch collectives,
+    torch.cuda.synchronize, the ctypes RCCL calls -- releases the GIL);
+    faulthandler's C timer, 30 s later, is the backstop for a call that does
+    not."""
+
+    def __init__(self, rank, world):
+        self.rank, self.world = rank, world
+        self.phase = "start"
+        self.phases = []
+        self.deadline = None
+        self._thread = None
+
+    def enter(self, phase):
+        self.phase = phase
+        self.phases.append([phase, round(time.monotonic() - T_START, 3)])
+
+    def arm(self, at):
+        """Fire at monotonic time `at` (None or <= T_START: off).  Ranks other
+        than 0 wait 5 s longer, so on a whole-job hang rank 0 reports first:
+        its status line is the one on stdout, and torchrun's SIGTERM then
+        dumps the others' stacks."""
+        if at is None or at <= T_START:
+            return
+        if self.rank != 0:
+            at += 5.0
+        self.deadline = at
+        faulthandler.dump_traceback_later(max(1.0, at - time.monotonic()) + 30.0, exit=True)
+        if self._thread is None:
+            self._thread = threading.Thread(target=self._run, name="bench-watchdog", daemon=True)
+            self._thread.start()
+
+    def cancel(self):
+        self.deadline = None
+        faulthandler.cancel_dump_traceback_later()
+
+    def _run(self):
+        while True:
+            time.sleep(0.25)
+            d = self.deadline
+            if d is not None and time.monotonic() >= d:
+                self.fire()
+
+    def fire(self):
+        line = status_line("watchdog", self.phase, self.rank, self.world, phases=self.phases)
+        print(json.dumps(line), file=sys.stdout if self.rank == 0 else sys.stderr, flush=True)
+        sys.stderr.write(f"bench: rank {self.rank}/{self.world}: watchdog after {line['elapsed_s']} s "
+                         f"in phase {self.phase!r}; Python stacks of every thread:\n")
+        sys.stderr.flush()
+        faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+        sys.stderr.flush()
+        os._exit(WATCHDOG_EXIT)
+
+
+def install_stack_dumps():
+    """Fatal signals and torchrun's SIGTERM (sent to the surviving ranks when
+    one fails) print every thread's Python stack before the process ends."""
+    faulthandler.enable(all_threads=True)
+    try:
+        faulthandler.register(signal.SIGTERM, all_threads=True, chain=True)
+    except (AttributeError, ValueError, RuntimeError):  # pragma: no cover - not on this platform
+        pass
+
+
+def pg_timeout(args):
+    return datetime.timedelta(seconds=max(1.0, args.pg_timeout_seconds))
+
+
+def remaining(args):
+    """Seconds left of --deadline-seconds."""
+    return T_START + args.deadline_seconds - time.monotonic()
 
 
 def _free_port():
@@ -201,12 +317,16 @@ def gather_stats(impl, world, B, ms):
     return out
 
 
-def cpu_baseline(procs, seconds):
+def cpu_baseline(procs, seconds, timeout=None):
     """float64 restatement of mano_np.py:81-115 on `procs` host cores (oracle/cpu_baseline.py,
     run as a child process so its workers share nothing with the GPU process)."""
-    r = subprocess.run([sys.executable, os.path.join(REPO, "oracle", "cpu_baseline.py"),
-                        "--procs", str(procs), "--seconds", str(seconds)],
-                       capture_output=True, text=True, timeout=120 + 4 * seconds)
+    try:
+        r = subprocess.run([sys.executable, os.path.join(REPO, "oracle", "cpu_baseline.py"),
+                            "--procs", str(procs), "--seconds", str(seconds)],
+                           capture_output=True, text=True,
+                           timeout=timeout if timeout is not None else 120 + 4 * seconds)
+    except subprocess.TimeoutExpired:
+        return {"value": None, "error": f"timed out after {timeout} s"}
     if r.returncode != 0:
         return {"value": None, "error": r.stderr[-500:]}
     res = json.loads(r.stdout.strip().splitlines()[-1])
@@ -276,8 +396,13 @@ def check_sample(model, seed, first, B, betas, pose, trans, verts, joints, model
     os.close(fd)
     try:
         np.savez(path, **arrays)
-        r = subprocess.run([sys.executable, os.path.join(REPO, "oracle", "check_sample.py"), path],
-                           capture_output=True, text=True, timeout=300)
+        # well inside --pg-timeout-seconds: the other ranks wait for this
+        # leg in the collective that merges the checks
+        try:
+            r = subprocess.run([sys.executable, os.path.join(REPO, "oracle", "check_sample.py"), path],
+                               capture_output=True, text=True, timeout=120)
+        except subprocess.TimeoutExpired:
+            return {"error": "oracle/check_sample.py timed out after 120 s"}
         if r.returncode != 0:
             return {"error": r.stderr[-500:]}
         res = json.loads(r.stdout.strip().splitlines()[-1])
@@ -430,21 +555,30 @@ def live_traffic(args, batch, name_fragment, timeout=120, local_dev=0):
                      "write_size_kb": kb["WRITE_SIZE"]}
 
 
-def launch_check(args):
-    """--launch-check: the N ranks meet over gloo and rank 0 prints the world (no GPU)."""
+def launch_check(args, wd):
+    """--launch-check: the N ranks meet over gloo and rank 0 prints the world
+    (no GPU).  With --inject-hang R, rank R skips the all_reduce and stalls:
+    the hang path of the watchdog / process-group timeout, tested on CPU."""
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if world > 1:
-        dist.init_process_group("gloo")
+        wd.enter("launch_check:init_process_group")
+        dist.init_process_group("gloo", timeout=pg_timeout(args))
         t = torch.tensor([rank], dtype=torch.int64)
+        wd.enter("launch_check:all_reduce")
+        if args.inject_hang == rank:
+            while True:       # a rank stuck outside the collective (e.g. in a kernel)
+                time.sleep(0.5)
         dist.all_reduce(t)
         total = int(t.item())
+        wd.enter("launch_check:barrier")
         dist.barrier()
         dist.destroy_process_group()
     else:
         total = 0
+    wd.cancel()
     if rank == 0:
         print(json.dumps({"launch_check": True, "n_gpus": world, "rank_sum": total,
                           "local_ranks_ok": total == world * (world - 1) // 2}), flush=True)
@@ -456,19 +590,39 @@ def main(argv=None):
     if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.force_pg):
         # Launch N ranks; this process never touches a GPU (it only waits).
         sys.exit(subprocess.run(launch_command(raw, args.gpus)).returncode)
-    if args.launch_check:
-        return launch_check(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    wd = Watchdog(rank, world)
+    guarded = world > 1 or args.force_pg
+    if guarded:
+        # A rank stuck in a collective (RCCL init, the gather, a barrier)
+        # prints its phase and every thread's Python stack and exits, so a
+        # first multi-GPU run that hangs leaves a diagnosis instead of a
+        # silent kill at the driver's limit.
+        install_stack_dumps()
+        # ties a SIGTERM stack dump (no rank in it) to torchrun's pid table
+        print(f"bench: rank {rank}/{world} pid {os.getpid()} local_rank "
+              f"{os.environ.get('LOCAL_RANK', '0')}", file=sys.stderr, flush=True)
+        if args.watchdog_seconds > 0:
+            wd.arm(T_START + args.watchdog_seconds)
+    try:
+        if args.launch_check:
+            return launch_check(args, wd)
+        return run(args, wd)
+    except Exception as e:
+        if guarded or rank == 0:
+            line = status_line("error", wd.phase, rank, world, error=f"{type(e).__name__}: {e}"[:500],
+                               phases=wd.phases)
+            print(json.dumps(line), file=sys.stdout if rank == 0 else sys.stderr, flush=True)
+        raise
 
+
+def run(args, wd):
+    """One benchmark run of this rank (main() holds the watchdog around it)."""
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.watchdog_seconds > 0 and (world > 1 or args.force_pg):
-        # A rank stuck in a collective (RCCL init, the gather, a barrier)
-        # prints every thread's Python stack and exits, so a first multi-GPU
-        # run that hangs leaves a diagnosis instead of a silent timeout.
-        import faulthandler
-        faulthandler.dump_traceback_later(args.watchdog_seconds, exit=True)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and args.gpus not in (1, world):
@@ -487,12 +641,20 @@ def main(argv=None):
     local_dev = local if args.backend == "nccl" else local % max(ndev, 1)
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
+    end_group = None
     if dist_on:
+        wd.enter("init_process_group")
         if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=pg_timeout(args))
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=pg_timeout(args))
+        # The last meeting of the run waits for rank 0's host legs (minutes of
+        # CPU work, no GPU): a gloo group whose timeout covers the deadline,
+        # so the RCCL group's short timeout never fires on a healthy run.
+        end_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(
+            seconds=max(60.0, args.deadline_seconds + 60.0)))
 
+    wd.enter("model_create")
     from mano_amd import ManoHip, load_dump, synthetic_params
     from mano_amd.distributed import AbiGather, all_gather, gather_to_root
     params = load_dump(args.model) if args.model else synthetic_params(0)
@@ -510,6 +672,7 @@ def main(argv=None):
     impl = args.gather_impl
     if gather_on:
         if args.backend == "nccl":
+            wd.enter("comm_create")
             gatherer = AbiGather(local_dev)
         if rank == 0 or impl == "allgather":
             # the assembled buffers (rank r's rows at r*B), allocated once: GPU 0's
@@ -586,6 +749,7 @@ def main(argv=None):
     # the C4 gather every step is a collective, and ranks that each read
     # their own clock could run different numbers of ramp steps -- the
     # unmatched gathers would hang.
+    wd.enter("ramp")
     t_ramp = time.perf_counter()
     n_ramp = 0
     while True:
@@ -602,6 +766,7 @@ def main(argv=None):
         if done:
             break
     t_ramp = time.perf_counter() - t_ramp
+    wd.enter("warmup")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -617,6 +782,7 @@ def main(argv=None):
     # the gather of the same sampled steps, bracketed on the same stream
     gevents = [[torch.cuda.Event(enable_timing=True) for _ in range(2)]
                if gather_on and i % every == 0 else None for i in range(args.steps)]
+    wd.enter("timed")
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
@@ -661,6 +827,7 @@ def main(argv=None):
     ms = {k: span(a, b, sampled) for k, (a, b) in timed[args.path].items()}
     other = {"fp32": "f16x3", "f16x3": "fp32"}[args.precision]
     ms_other = {}
+    wd.enter("kernel_table")
     if rank == 0 and not args.no_extra:
         scratch = (torch.empty_like(verts), torch.empty_like(joints))
 
@@ -700,6 +867,7 @@ def main(argv=None):
     # The other gather form (report both), timed after the
     # timed region on every rank the same way; its buffers are freed after.
     if gather_on and gatherer is not None and args.gather_compare_reps > 0:
+        wd.enter("gather_compare")
         other_impl = "allgather" if impl == "sendrecv" else "sendrecv"
         keep = (gv, gj)
         if other_impl == "allgather" or rank == 0:
@@ -756,8 +924,13 @@ def main(argv=None):
                                  "bound": "mfma", "achieved_TFLOPs": a,
                                  "frac": a / PEAK_FP32_TFLOPS,
                                  "flop_per_hand": FUSED_FLOP_PER_HAND,
+                                 "flop_basis": ("SURVEY.md §8(d): blend GEMM 2x2334x145 + LBS 778x405 "
+                                                "(transform blend on MFMA + the 21-flop apply on the VALU, "
+                                                "the same fp32 datapath and peak on gfx950)"),
                                  "mfma_only": {"flop_per_hand": FUSED_MFMA_FLOP_PER_HAND, "achieved_TFLOPs": a_mfma,
-                                               "frac": a_mfma / PEAK_FP32_TFLOPS},
+                                               "frac": a_mfma / PEAK_FP32_TFLOPS,
+                                               "flop_basis": "MFMA flops only: GEMM + the 16-joint transform "
+                                                             "blend (rounds 1-3's numerator; compare rounds on this)"},
                                  "blend_gemm_TFLOPs": tflops(BLEND_FLOP_PER_HAND, ms["blend_skin"])}
     elif "blend_skin" in ms:  # f16x3: the split GEMM runs at 16/3 x the fp32 rate; HBM stores bound it
         a = gbs(FUSED_BYTES_PER_HAND, ms["blend_skin"])
@@ -819,6 +992,8 @@ def main(argv=None):
             roof = {"kernel": kd["kernel"], "bound": "hbm", "achieved": kd["achieved_GBs"],
                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": kd["frac"]}
         roof["algorithmic_per_hand"] = kd.get("flop_per_hand", kd.get("bytes_per_hand"))
+        if "flop_basis" in kd:
+            roof["flop_basis"] = kd["flop_basis"]
         if "mfma_only" in kd:  # the same launches counted with the MFMA flops alone (rounds 1-3's numerator)
             roof["mfma_only"] = kd["mfma_only"]
         roof["hands_per_launch"] = B
@@ -830,6 +1005,7 @@ def main(argv=None):
     # gather, GPU 0's assembled buffers vs a local forward of hands
     # regenerated by global index from every rank's range.
     correctness, gather_check = None, None
+    wd.enter("correctness")
     device_status = model.device_status(clear=True)  # MANO_DEVICE_* bits raised by any launch (0 = none)
     if not args.no_check:
         correctness = check_sample(model, wl["seed"], rank * B, B, betas, pose, trans, verts, joints,
@@ -851,17 +1027,31 @@ def main(argv=None):
         if args.dump_gather:
             np.savez(args.dump_gather, verts=gv.cpu().numpy(), joints=gj.cpu().numpy())
 
+    # The collective phases are over.  Rank 0's host legs hold no collective
+    # and each is bounded by its own child timeout, fitted into the deadline;
+    # the other ranks wait for them at the gloo end barrier.  From here the
+    # watchdog fires only past the deadline (+30 s, inside the driver's lease).
+    wd.enter("rank0_legs" if rank == 0 else "end_barrier")
+    if dist_on and args.watchdog_seconds > 0:
+        wd.arm(T_START + args.deadline_seconds + 30.0)
+
     # Rank 0's host-side legs, at every N (the other ranks wait at a barrier,
     # their GPUs idle): roofline.traffic by two rocprofv3 --pmc passes over a
     # child run on rank 0's GPU only, the drop-in latency, the CPU baseline.
-    extra = {}
+    extra, skipped = {}, {}
     if rank == 0:
         if roof is not None:
             traffic, src, live = None, None, None
             if not args.no_live_pmc:
                 frag = PMC_KERNEL_NAME.get(dominant + ("_h3" if args.precision == "f16x3" else ""))
-                if frag is not None:
-                    traffic, live = live_traffic(args, B, frag, local_dev=local_dev)
+                left = remaining(args)
+                if left < 100:
+                    live = f"skipped: {left:.0f} s left of --deadline-seconds"
+                    skipped["live_pmc"] = live
+                elif frag is not None:
+                    wd.enter("rank0_legs:live_pmc")
+                    traffic, live = live_traffic(args, B, frag, local_dev=local_dev,
+                                                 timeout=min(120.0, (left - 60.0) / 2.0))
                     if traffic is not None:
                         src = (f"measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over "
                                f"a 3-step 1-rank child run at {B} hands on rank 0's GPU (read = 2 x FETCH_SIZE)"
@@ -875,26 +1065,46 @@ def main(argv=None):
             roof["traffic_source"] = src
             if isinstance(live, dict):
                 roof["traffic_detail"] = live
+            if traffic is not None and kernels.get(dominant, {}).get("ms"):
+                # the HBM side of the same launches (north_star: "MFMA and HBM rooflines")
+                hbm = traffic / (kernels[dominant]["ms"] * 1e-3) / 1e9
+                roof["hbm_GBs"] = hbm
+                roof["hbm_frac"] = hbm / PEAK_HBM_GBS
         if not args.no_dropin:
-            extra["dropin"] = dropin_latency(params, local_dev)
+            if remaining(args) < 40:
+                skipped["dropin"] = f"{remaining(args):.0f} s left of --deadline-seconds"
+            else:
+                wd.enter("rank0_legs:dropin")
+                extra["dropin"] = dropin_latency(params, local_dev)
         if not args.no_cpu:
-            procs = args.cpu_procs or cpu_share(world)
-            cb = cpu_baseline(procs, args.cpu_seconds)
-            if world > 1:
-                cb["note"] = (f"rank 0 after the timed region while the other {world - 1} ranks wait at a "
-                              f"barrier; {procs} of this node's cores")
-            extra["cpu_baseline"] = cb
-            if "dropin" in extra and cb.get("value"):
-                # the per-hand port's time per hand on ONE core (the reference's
-                # own loop runs at 1/1.055 of it: profiles/cpu_calibration.json)
-                extra["dropin"]["cpu_port_us_per_hand_one_core"] = cb["cores"] / cb["value"] * 1e6
+            # two forms of `secs` each plus process start-up must end 20 s
+            # before the deadline
+            secs = min(args.cpu_seconds, (remaining(args) - 50.0) / 2.5)
+            if secs < 1.0:
+                skipped["cpu_baseline"] = f"{remaining(args):.0f} s left of --deadline-seconds"
+            else:
+                wd.enter("rank0_legs:cpu_baseline")
+                procs = args.cpu_procs or cpu_share(world)
+                cb = cpu_baseline(procs, round(secs, 1), timeout=max(10.0, remaining(args) - 20.0))
+                if secs < args.cpu_seconds:
+                    cb["shortened"] = f"{secs:.1f} s per form (of {args.cpu_seconds}) to fit --deadline-seconds"
+                if world > 1:
+                    cb["note"] = (f"rank 0 after the timed region while the other {world - 1} ranks wait at a "
+                                  f"barrier; {procs} of this node's cores")
+                extra["cpu_baseline"] = cb
+                if "dropin" in extra and cb.get("value"):
+                    # the per-hand port's time per hand on ONE core (the reference's
+                    # own loop runs at 1/1.055 of it: profiles/cpu_calibration.json)
+                    extra["dropin"]["cpu_port_us_per_hand_one_core"] = cb["cores"] / cb["value"] * 1e6
     if dist_on:
-        dist.barrier()
+        wd.enter("end_barrier")
+        dist.barrier(group=end_group)
+    wd.cancel()
 
     if rank == 0:
         total = B * world * args.steps
         line = {
-            "metric": "posed hand meshes/sec (whole node)",
+            "metric": METRIC,
             "value": total / dt,
             "unit": "hands/s",
             "n_gpus": world,
@@ -931,6 +1141,12 @@ def main(argv=None):
         if gather_check is not None:
             line["gather_check"] = gather_check
         line.update(extra)
+        line["status"] = "ok"
+        line["run"] = {"wall_s": round(time.monotonic() - T_START, 3), "phases": wd.phases,
+                       "deadline_s": args.deadline_seconds,
+                       "watchdog_s": args.watchdog_seconds if dist_on else None,
+                       "pg_timeout_s": args.pg_timeout_seconds if dist_on else None,
+                       "skipped_legs": skipped}
         print(json.dumps(line), flush=True)
     if gatherer is not None:
         gatherer.close()

@@ -8,6 +8,7 @@ import json
 import os
 import subprocess
 import sys
+import time
 
 import pytest
 
@@ -29,6 +30,60 @@ def test_gpus_flag_launches_n_ranks(n):
     assert r.returncode == 0, r.stderr[-2000:]
     line = _last_json(r.stdout)
     assert line["n_gpus"] == n and line["local_ranks_ok"]
+
+
+def test_failure_budgets_inside_driver_lease():
+    """The driver kills a bench run at 600 s: a stalled collective must raise
+    (process-group timeout) before the watchdog fires, the watchdog before the
+    lease ends, and rank 0's host legs end by the deadline (the re-armed
+    watchdog at deadline + 30 s still inside 600 s)."""
+    a = bench.parse([])
+    assert 0 < a.pg_timeout_seconds < a.watchdog_seconds < 600
+    assert a.watchdog_seconds <= a.deadline_seconds and a.deadline_seconds + 30 < 600
+    # a shard's oracle check (the collective that merges them waits for it) is
+    # bounded well inside the process-group timeout: bench.check_sample uses 120 s
+    assert 120 < a.pg_timeout_seconds
+
+
+def _hang_run(extra):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                        "--launch-check", "--inject-hang", "1", *extra],
+                       capture_output=True, text=True, timeout=240, env=env)
+    return r, time.monotonic() - t0
+
+
+def test_hang_path_watchdog_names_phase_and_dumps_both_ranks():
+    """Rank 1 stalls outside the all_reduce rank 0 waits in (longer PG timeout):
+    both watchdogs fire, rank 0 prints the status line with the phase, both
+    ranks' Python stacks reach stderr, the launcher exits non-zero -- well
+    inside the default watchdog."""
+    r, wall = _hang_run(["--watchdog-seconds", "12", "--pg-timeout-seconds", "200"])
+    assert r.returncode != 0
+    line = _last_json(r.stdout)
+    assert line["status"] == "watchdog" and line["value"] is None and line["rank"] == 0
+    assert line["phase"] == "launch_check:all_reduce"
+    # rank 0 fires first (the others allow it a grace period); rank 1's stack
+    # comes from its own watchdog or from torchrun's SIGTERM after rank 0 exits
+    assert "rank 0/2: watchdog" in r.stderr
+    assert r.stderr.count("in launch_check") >= 2          # both main threads' stacks
+    assert "in all_reduce" in r.stderr                      # rank 0 was inside the collective
+    assert wall < bench.parse([]).watchdog_seconds
+
+
+def test_hang_path_pg_timeout_raises_and_peer_stack_dumped():
+    """Process-group timeout shorter than the watchdog: rank 0's collective
+    raises, its status line says "error" in the phase, and torchrun's SIGTERM
+    to the stalled rank dumps that rank's stack."""
+    r, wall = _hang_run(["--watchdog-seconds", "100", "--pg-timeout-seconds", "5"])
+    assert r.returncode != 0
+    line = _last_json(r.stdout)
+    assert line["status"] == "error" and line["phase"] == "launch_check:all_reduce"
+    assert "Timed out" in line["error"] or "timeout" in line["error"].lower()
+    assert r.stderr.count("in launch_check") >= 2           # rank 0's traceback + rank 1's SIGTERM dump
+    assert "bench: rank 1/2 pid" in r.stderr
+    assert wall < 100
 
 
 def test_launch_command_is_torchrun():
