@@ -46,6 +46,8 @@ extern "C" {
 #define MANO_ESMALL (-3)   /* workspace smaller than mano_workspace_bytes()     */
 #define MANO_ESTATE (-4)   /* handle destroyed / wrong device                   */
 #define MANO_ECOMM (-5)    /* RCCL unavailable or a collective failed           */
+#define MANO_EDEVICE (-6)  /* an earlier launch on this model raised a MANO_DEVICE_* bit:
+                              its outputs are not valid (mano_model_device_status) */
 
 #define MANO_N_JOINTS 16
 #define MANO_N_SHAPE 10
@@ -101,19 +103,27 @@ int mano_model_destroy(mano_model* model);
 /* Vertex count and device of a model. */
 int mano_model_info(const mano_model* model, int32_t* n_verts, int32_t* device);
 
-/* Device status word of a model: MANO_DEVICE_* bits raised by kernels since
- * the last clear.  Waits for every launch on the model's device first
- * (hipDeviceSynchronize), reads the word into *status and, with `clear`
- * non-zero, resets it -- the read and the reset are one device atomic, so a
- * bit raised by a launch from another thread is reported by this call or by
- * the next, never dropped.  A non-zero word means some launch's outputs are
- * not valid:
+/* Device status of a model: the MANO_DEVICE_* bits kernels raised since the
+ * last clear.  A set bit means some launch's outputs are not valid:
  *   MANO_DEVICE_SKIN_HANDOFF_TIMEOUT  the standalone LBS (mano_stage_skin) lost
  *     a hand-over between its memory and compute waves (a bounded LDS wait
- *     gave up); the verts of the units it could not confirm were not
- *     written. */
+ *     gave up -- reachable only through a broken protocol: the waves of a
+ *     workgroup are co-resident); the verts of the units it could not
+ *     confirm were not written.
+ * Contract: launches are asynchronous, so the call that issued such a launch
+ * has already returned MANO_OK; from the moment the bit is raised, EVERY
+ * launching call on the model (mano_forward*, mano_stage_*,
+ * mano_pose_from_pca) returns MANO_EDEVICE without launching, until this
+ * function is called with MANO_STATUS_CLEAR.  The bits are flags in pinned
+ * host memory that the kernels set with plain stores: this call waits for
+ * every launch on the model's device (hipDeviceSynchronize; not with
+ * MANO_STATUS_NO_WAIT, which reads what has landed so far), ORs them into
+ * *status and, with MANO_STATUS_CLEAR, takes each with one host atomic
+ * exchange -- concurrent callers never lose a bit, each reports it once. */
 #define MANO_DEVICE_SKIN_HANDOFF_TIMEOUT 1
-int mano_model_device_status(const mano_model* model, int32_t* status, int32_t clear);
+#define MANO_STATUS_CLEAR 1
+#define MANO_STATUS_NO_WAIT 2
+int mano_model_device_status(const mano_model* model, int32_t* status, int32_t flags);
 
 /* Device workspace (bytes) for n_hands: `mano_workspace_bytes` covers every
  * call (the unfused stages keep v_posed in it); `mano_forward_workspace_bytes`
@@ -256,6 +266,18 @@ int mano_comm_create(int device, int32_t n_ranks, int32_t rank, const unsigned c
 int mano_comm_destroy(mano_comm* comm);
 int mano_gather(mano_comm* comm, const void* send, size_t send_bytes, void* recv,
                 const size_t* rank_bytes, int32_t root, void* stream);
+/* Single-process form (ABI 6): ONE host thread drives n devices, as the
+ * reference's own single-process batch loop would (data_explore.py:12-15;
+ * ncclCommInitAll).  mano_comm_create_all makes one
+ * communicator per device in one call (rank i on devices[i], distinct
+ * devices; comms[n] out).  Calls on several of them from one thread go
+ * between mano_group_start and mano_group_end (ncclGroupStart / End), which
+ * issues them together: mano_gather on every comm with its own send buffer
+ * and stream (recv on the root's) gathers all devices' shards onto the root
+ * without any other thread or process.  Each comm is destroyed on its own. */
+int mano_comm_create_all(int32_t n, const int* devices, mano_comm** comms);
+int mano_group_start(void);
+int mano_group_end(void);
 /* Every rank receives every shard: RCCL's ring ncclAllGather of equal
  * `send_bytes` shards, rank r's bytes at recv + r * send_bytes on EVERY rank
  * (recv holds n_ranks * send_bytes; in place when send == recv + rank *
@@ -269,7 +291,10 @@ int mano_allgather(mano_comm* comm, const void* send, size_t send_bytes, void* r
 /* Message of the last failed call on this thread ("" if none). */
 const char* mano_last_error(void);
 
-/* ABI version, bumped on any signature change (4: + mano_allgather; 5: + mano_host_alloc / mano_host_free). */
+/* ABI version, bumped on any signature change (4: + mano_allgather; 5: +
+ * mano_host_alloc / mano_host_free; 6: + mano_comm_create_all /
+ * mano_group_start / mano_group_end, MANO_EDEVICE, mano_model_device_status
+ * flags). */
 int mano_abi_version(void);
 
 #ifdef __cplusplus

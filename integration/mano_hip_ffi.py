@@ -34,6 +34,7 @@ LIB_PATH = os.environ.get(
 _p, _i32, _i64, _sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
 _d = ctypes.POINTER(ctypes.c_double)
 H2D, D2H = 1, 2  # MANO_MEMCPY_HOST_TO_DEVICE, MANO_MEMCPY_DEVICE_TO_HOST
+STATUS_NO_WAIT = 2  # MANO_STATUS_NO_WAIT
 N_JOINTS, N_SHAPE = 16, 10
 
 _lib = ctypes.CDLL(LIB_PATH)
@@ -49,6 +50,7 @@ for _name, _res, _args in (
         ("mano_host_alloc", ctypes.c_int, [_sz, ctypes.POINTER(_p)]),
         ("mano_host_free", ctypes.c_int, [_p]),
         ("mano_synchronize", ctypes.c_int, [ctypes.c_int]),
+        ("mano_model_device_status", ctypes.c_int, [_p, ctypes.POINTER(_i32), _i32]),
         ("mano_last_error", ctypes.c_char_p, [])):
     _fn = getattr(_lib, _name)
     _fn.restype, _fn.argtypes = _res, _args
@@ -156,18 +158,30 @@ class Engine:
                                  b["joints"], b["rest_verts"], b["rest_joints"], b["rot_mats"],
                                  b["workspace"], self._ws_bytes, None))
         V = self.n_verts
+        shapes = {"verts": (B, V, 3), "J": ("rest_joints", (B, N_JOINTS, 3)),
+                  "R": ("rot_mats", (B, N_JOINTS, 3, 3)), "rest_verts": (B, V, 3), "joints": (B, N_JOINTS, 3)}
+        shapes = {k: (v if isinstance(v[0], str) else (k, v)) for k, v in shapes.items()}
         if self.zero_copy:  # the outputs are in the host block once the launches completed
             _check(_lib.mano_synchronize(self.device))
-            out = self._out_block.astype(np.float64)  # one conversion, then views of it
-            at = self._out_at
-            view = lambda name, shape: out[at[name]:at[name] + int(np.prod(shape))].reshape(shape)  # noqa: E731
-            return {"verts": view("verts", (B, V, 3)), "J": view("rest_joints", (B, N_JOINTS, 3)),
-                    "R": view("rot_mats", (B, N_JOINTS, 3, 3)), "rest_verts": view("rest_verts", (B, V, 3)),
-                    "joints": view("joints", (B, N_JOINTS, 3))}
-        return {"verts": self._get("verts", (B, V, 3)), "J": self._get("rest_joints", (B, N_JOINTS, 3)),
-                "R": self._get("rot_mats", (B, N_JOINTS, 3, 3)),
-                "rest_verts": self._get("rest_verts", (B, V, 3)),
-                "joints": self._get("joints", (B, N_JOINTS, 3))}
+            self._check_status()
+            if B == self.capacity:
+                # the whole output region is this call's: one conversion, then views of it
+                out = self._out_block.astype(np.float64)
+                at = self._out_at
+                return {k: out[at[n]:at[n] + int(np.prod(s))].reshape(s) for k, (n, s) in shapes.items()}
+            # B < capacity: only each output's first B rows (cost follows B, not capacity)
+            return {k: self._get(n, s) for k, (n, s) in shapes.items()}
+        out = {k: self._get(n, s) for k, (n, s) in shapes.items()}
+        self._check_status()
+        return out
+
+    def _check_status(self):
+        """The kernels finished: raise if one raised a MANO_DEVICE_* bit (its
+        outputs are not valid; include/mano_hip.h mano_model_device_status)."""
+        st = _i32(0)
+        _check(_lib.mano_model_device_status(self._h, ctypes.byref(st), STATUS_NO_WAIT))
+        if st.value:
+            raise RuntimeError(f"libmano_hip: device status 0x{st.value:x}: outputs not valid")
 
     def close(self):
         if self._h:

@@ -23,7 +23,8 @@ struct mano_model {
   uint32_t magic;
   int device;
   mano::DeviceModel dm;
-  void* block;  // single device allocation holding every array of dm
+  void* block;            // single device allocation holding every array of dm
+  int32_t* status_flags;  // [kStatusFlags] pinned host memory; dm.status is its device address
 };
 
 namespace {
@@ -65,6 +66,33 @@ int check_model(const mano_model* m) {
   return MANO_OK;
 }
 
+// OR of the raised MANO_DEVICE_* bits (host reads of the pinned flags; no
+// wait).  `clear`: each flag is taken with one host atomic exchange, so a
+// flag a kernel sets after the exchange stays for the next reader.
+int32_t read_flags(const mano_model* m, bool clear) {
+  int32_t bits = 0;
+  for (int b = 0; b < mano::kStatusFlags; ++b) {
+    int32_t* f = m->status_flags + b;
+    const int32_t v = clear ? __atomic_exchange_n(f, 0, __ATOMIC_ACQ_REL) : __atomic_load_n(f, __ATOMIC_ACQUIRE);
+    if (v) bits |= int32_t(1) << b;
+  }
+  return bits;
+}
+
+// Every launching entry point on a model: a kernel of an earlier launch
+// raised a status flag, so its outputs are not valid -- fail loudly until the
+// caller has read (and cleared) the flags.
+int check_launchable(const mano_model* m) {
+  if (int rc = check_model(m)) return rc;
+  if (const int32_t bits = read_flags(m, false))
+    return fail(MANO_EDEVICE,
+                "device status 0x%x: an earlier launch on this model did not write all its outputs "
+                "(MANO_DEVICE_SKIN_HANDOFF_TIMEOUT = 1); mano_model_device_status with MANO_STATUS_CLEAR "
+                "reads and clears it",
+                unsigned(bits));
+  return MANO_OK;
+}
+
 // `full`: the unfused stages need the v_posed region too; the fused forward
 // only the feature tiles and skinning transforms.
 int check_workspace(const mano_model* m, int64_t n, const void* ws, size_t ws_bytes,
@@ -94,7 +122,7 @@ int set_error(int code, const char* msg) {
 
 extern "C" {
 
-int mano_abi_version(void) { return 5; }
+int mano_abi_version(void) { return 6; }
 
 const char* mano_last_error(void) { return g_last_error.c_str(); }
 
@@ -135,7 +163,7 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
 
   // ---- one device block, 256-B aligned sub-arrays ----
   struct Part { const void* src; size_t bytes; size_t off; };
-  enum { kBasis, kWeights, kJt, kJs, kParents, kDepth, kPcaB, kPcaM, kZeros, kStatus, kBasis16, kW16, kBasisH3, kB16V, kW16V, kTilesV, kBh3V, kNParts };
+  enum { kBasis, kWeights, kJt, kJs, kParents, kDepth, kPcaB, kPcaM, kZeros, kBasis16, kW16, kBasisH3, kB16V, kW16V, kTilesV, kBh3V, kNParts };
   std::vector<Part> parts(kNParts);
   parts[kBasis] = {hm.tiles.data(), hm.tiles.size() * 4, 0};
   parts[kWeights] = {hm.weights.data(), hm.weights.size() * 4, 0};
@@ -146,7 +174,6 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   parts[kPcaB] = {hm.pca.data(), hm.pca.size() * 4, 0};
   parts[kPcaM] = {hm.pmean.data(), hm.pmean.size() * 4, 0};
   parts[kZeros] = {zeros.data(), zeros.size() * 4, 0};
-  parts[kStatus] = {zeros.data(), 8, 0};  // [0] the status word, [1] its snapshot (device_status)
   parts[kBasis16] = {hm.b16.data(), hm.b16.size() * 4, 0};
   parts[kW16] = {hm.w16.data(), hm.w16.size() * 4, 0};
   parts[kBasisH3] = {hm.bh3.data(), hm.bh3.size() * 2, 0};
@@ -170,15 +197,29 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
       return hip_fail(e, "hipMemcpy(model buffer)");
     }
   }
-  mano_model* m = new (std::nothrow) mano_model();
-  if (!m) {
+  // The status flags: pinned, coherent host memory the kernels write
+  // through its device address (read by the host without a device copy).
+  void* flags = nullptr;
+  e = hipHostMalloc(&flags, kStatusFlags * sizeof(int32_t), hipHostMallocCoherent);
+  if (e != hipSuccess) {
     (void)hipFree(block);
-    return fail(MANO_EINVAL, "out of host memory");
+    return hip_fail(e, "hipHostMalloc(status flags)");
+  }
+  std::memset(flags, 0, kStatusFlags * sizeof(int32_t));
+  void* flags_dev = nullptr;
+  e = hipHostGetDevicePointer(&flags_dev, flags, 0);
+  mano_model* m = e == hipSuccess ? new (std::nothrow) mano_model() : nullptr;
+  if (!m) {
+    (void)hipHostFree(flags);
+    (void)hipFree(block);
+    return e != hipSuccess ? hip_fail(e, "hipHostGetDevicePointer(status flags)")
+                           : fail(MANO_EINVAL, "out of host memory");
   }
   char* b = static_cast<char*>(block);
   m->magic = kMagic;
   m->device = device;
   m->block = block;
+  m->status_flags = static_cast<int32_t*>(flags);
   auto at = [&](int i) { return reinterpret_cast<float*>(b + parts[i].off); };
   m->dm.basis_tiles = at(kBasis);
   m->dm.basis_tiles_v = hm.tiles_v.empty() ? nullptr : at(kTilesV);
@@ -190,7 +231,7 @@ int mano_model_create(int device, int32_t n_verts, const double* mesh_template,
   m->dm.pca_basis = at(kPcaB);
   m->dm.pca_mean = at(kPcaM);
   m->dm.zeros = at(kZeros);
-  m->dm.status = reinterpret_cast<int32_t*>(at(kStatus));
+  m->dm.status = static_cast<int32_t*>(flags_dev);
   m->dm.basis16 = at(kBasis16);
   m->dm.wfrag16 = at(kW16);
   m->dm.basis16v = hm.b16v.empty() ? nullptr : at(kB16V);
@@ -218,8 +259,10 @@ int mano_model_destroy(mano_model* m) {
   DeviceGuard guard(m->device);
   m->magic = 0;
   hipError_t e = hipFree(m->block);
+  const hipError_t ef = hipHostFree(m->status_flags);
   delete m;
   if (e != hipSuccess) return hip_fail(e, "hipFree(model buffer)");
+  if (ef != hipSuccess) return hip_fail(ef, "hipHostFree(status flags)");
   return MANO_OK;
 }
 
@@ -248,37 +291,24 @@ int mano_model_get_precision(const mano_model* m, int32_t* precision) {
 
 }  // extern "C"
 
-namespace {
-// mano_model_device_status's read (and clear) of the status word as ONE
-// device atomic, so a bit a kernel on another stream or thread raises
-// between the read and the clear is never lost: it lands either in the
-// snapshot or, after the exchange, in the word for the next call.
-__global__ void status_take_kernel(int32_t* word, int32_t clear) {
-  if (threadIdx.x == 0) {
-    int32_t v = clear ? __hip_atomic_exchange(word, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                      : __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    word[1] = v;  // plain vector store of the snapshot
-  }
-}
-}  // namespace
-
 extern "C" {
 
-int mano_model_device_status(const mano_model* m, int32_t* status, int32_t clear) {
+int mano_model_device_status(const mano_model* m, int32_t* status, int32_t flags) {
   g_last_error.clear();
   if (int rc = check_model(m)) return rc;
   if (!status) return fail(MANO_EINVAL, "status is NULL");
-  DeviceGuard guard(m->device);
-  if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
-  hipError_t e = hipDeviceSynchronize();
-  if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
-  hipLaunchKernelGGL(status_take_kernel, dim3(1), dim3(64), 0, nullptr, m->dm.status, clear ? 1 : 0);
-  e = hipGetLastError();
-  if (e != hipSuccess) return hip_fail(e, "status_take_kernel launch");
-  int32_t word = 0;
-  e = hipMemcpy(&word, m->dm.status + 1, sizeof(word), hipMemcpyDeviceToHost);  // after the kernel (null stream)
-  if (e != hipSuccess) return hip_fail(e, "hipMemcpy(status)");
-  *status = word;
+  if (flags & ~(MANO_STATUS_CLEAR | MANO_STATUS_NO_WAIT))
+    return fail(MANO_EINVAL, "flags 0x%x: only MANO_STATUS_CLEAR | MANO_STATUS_NO_WAIT", unsigned(flags));
+  if (!(flags & MANO_STATUS_NO_WAIT)) {
+    DeviceGuard guard(m->device);
+    if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
+  }
+  // Host reads of the pinned flags: each call takes its own snapshot (no
+  // shared device slot, no copy), and with CLEAR each flag goes through one
+  // host atomic exchange -- concurrent callers never lose a bit.
+  *status = read_flags(m, flags & MANO_STATUS_CLEAR);
   return MANO_OK;
 }
 
@@ -307,7 +337,7 @@ int mano_stage_articulate(const mano_model* m, int64_t n, const float* betas,
                           int64_t betas_stride, const float* pose, const float* trans,
                           float* joints, float* rest_joints, float* rot_mats, void* ws,
                           size_t ws_bytes, void* stream) {
-  if (int rc = check_model(m)) return rc;
+  if (int rc = check_launchable(m)) return rc;
   if (n < 0 || n > kMaxHands) return fail(MANO_EINVAL, "n_hands %lld out of range", (long long)n);
   if (n == 0) return MANO_OK;
   if (!betas || !pose) return fail(MANO_EINVAL, "betas and pose are required");
@@ -328,7 +358,7 @@ int mano_stage_articulate(const mano_model* m, int64_t n, const float* betas,
 
 int mano_stage_blend(const mano_model* m, int64_t n, float* rest_verts, void* ws, size_t ws_bytes,
                      void* stream) {
-  if (int rc = check_model(m)) return rc;
+  if (int rc = check_launchable(m)) return rc;
   if (n < 0 || n > kMaxHands) return fail(MANO_EINVAL, "n_hands %lld out of range", (long long)n);
   if (n == 0) return MANO_OK;
   if (int rc = check_workspace(m, n, ws, ws_bytes)) return rc;
@@ -345,7 +375,7 @@ int mano_stage_blend(const mano_model* m, int64_t n, float* rest_verts, void* ws
 
 int mano_stage_skin(const mano_model* m, int64_t n, const float* rest_verts, const float* trans,
                     float* verts, void* ws, size_t ws_bytes, void* stream) {
-  if (int rc = check_model(m)) return rc;
+  if (int rc = check_launchable(m)) return rc;
   if (n < 0 || n > kMaxHands) return fail(MANO_EINVAL, "n_hands %lld out of range", (long long)n);
   if (n == 0) return MANO_OK;
   if (!verts) return fail(MANO_EINVAL, "verts is required");
@@ -365,7 +395,7 @@ int mano_stage_skin(const mano_model* m, int64_t n, const float* rest_verts, con
 
 int mano_stage_blend_skin(const mano_model* m, int64_t n, float* rest_verts, const float* trans,
                           float* verts, void* ws, size_t ws_bytes, void* stream) {
-  if (int rc = check_model(m)) return rc;
+  if (int rc = check_launchable(m)) return rc;
   if (n < 0 || n > kMaxHands) return fail(MANO_EINVAL, "n_hands %lld out of range", (long long)n);
   if (n == 0) return MANO_OK;
   if (!verts) return fail(MANO_EINVAL, "verts is required");
@@ -389,7 +419,7 @@ int mano_forward(const mano_model* m, int64_t n, const float* betas, int64_t bet
                  float* rest_verts, float* rest_joints, float* rot_mats, void* ws,
                  size_t ws_bytes, void* stream) {
   g_last_error.clear();
-  if (int rc = check_model(m)) return rc;
+  if (int rc = check_launchable(m)) return rc;
   if (n > 0 && !verts) return fail(MANO_EINVAL, "verts is required");
   if (int rc = mano_stage_articulate(m, n, betas, betas_stride, pose, trans, joints, rest_joints,
                                      rot_mats, ws, ws_bytes, stream))
@@ -400,7 +430,7 @@ int mano_forward(const mano_model* m, int64_t n, const float* betas, int64_t bet
 int mano_pose_from_pca(const mano_model* m, int64_t n, const float* pca, int32_t n_comps,
                        int64_t pca_stride, const float* rot, int64_t rot_stride, float* pose,
                        void* stream) {
-  if (int rc = check_model(m)) return rc;
+  if (int rc = check_launchable(m)) return rc;
   if (n < 0 || n > kMaxHands) return fail(MANO_EINVAL, "n_hands %lld out of range", (long long)n);
   if (n_comps < 0 || n_comps > mano::kPca)
     return fail(MANO_EINVAL, "n_comps %d must be in [0, 45] (mano_np.py:55-56)", n_comps);
@@ -425,7 +455,7 @@ int mano_forward_pca(const mano_model* m, int64_t n, const float* betas, int64_t
                      float* pose_out, float* rest_verts, float* rest_joints, float* rot_mats,
                      void* ws, size_t ws_bytes, void* stream) {
   g_last_error.clear();
-  if (int rc = check_model(m)) return rc;
+  if (int rc = check_launchable(m)) return rc;
   if (n < 0 || n > kMaxHands) return fail(MANO_EINVAL, "n_hands %lld out of range", (long long)n);
   if (!m->dm.has_pca) return fail(MANO_EINVAL, "the model was created without the PCA arrays");
   if (n_comps < 0 || n_comps > mano::kPca)

@@ -73,6 +73,7 @@ struct Rccl {
   std::string why;
   decltype(&ncclGetUniqueId) get_unique_id = nullptr;
   decltype(&ncclCommInitRank) init_rank = nullptr;
+  decltype(&ncclCommInitAll) init_all = nullptr;
   decltype(&ncclCommDestroy) destroy = nullptr;
   decltype(&ncclSend) send = nullptr;
   decltype(&ncclRecv) recv = nullptr;
@@ -99,6 +100,7 @@ const Rccl& rccl() {
     };
     r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(sym("ncclGetUniqueId"));
     r.init_rank = reinterpret_cast<decltype(r.init_rank)>(sym("ncclCommInitRank"));
+    r.init_all = reinterpret_cast<decltype(r.init_all)>(sym("ncclCommInitAll"));
     r.destroy = reinterpret_cast<decltype(r.destroy)>(sym("ncclCommDestroy"));
     r.send = reinterpret_cast<decltype(r.send)>(sym("ncclSend"));
     r.recv = reinterpret_cast<decltype(r.recv)>(sym("ncclRecv"));
@@ -175,6 +177,65 @@ int mano_comm_create(int device, int32_t n_ranks, int32_t rank, const unsigned c
     return fail(MANO_EINVAL, "out of host memory");
   }
   *out = c;
+  return MANO_OK;
+}
+
+int mano_comm_create_all(int32_t n, const int* devices, mano_comm** comms) {
+  mano::set_error(MANO_OK, "");
+  if (!comms) return fail(MANO_EINVAL, "comms is NULL");
+  if (n < 1) return fail(MANO_EINVAL, "n %d < 1", n);
+  for (int i = 0; i < n; ++i) comms[i] = nullptr;
+  if (!devices) return fail(MANO_EINVAL, "devices is NULL");
+  int n_dev = 0;
+  hipError_t he = hipGetDeviceCount(&n_dev);
+  if (he != hipSuccess) return fail(MANO_EHIP, "hipGetDeviceCount: %s", hipGetErrorString(he));
+  for (int i = 0; i < n; ++i) {
+    if (devices[i] < 0 || devices[i] >= n_dev)
+      return fail(MANO_EINVAL, "devices[%d] = %d outside [0, %d)", i, devices[i], n_dev);
+    for (int j = 0; j < i; ++j)
+      if (devices[j] == devices[i])
+        return fail(MANO_EINVAL, "device %d is listed twice (one communicator rank per GPU)", devices[i]);
+  }
+  const Rccl& r = rccl();
+  if (!r.ok) return fail(MANO_ECOMM, "%s", r.why.c_str());
+  std::vector<ncclComm_t> raw(n, nullptr);
+  {
+    DeviceGuard guard(devices[0]);  // ncclCommInitAll sets each device itself; restore the caller's
+    ncclResult_t res = r.init_all(raw.data(), n, devices);  // one clique, rank i on devices[i]
+    if (res != ncclSuccess) return rccl_fail(r, res, "ncclCommInitAll");
+  }
+  for (int i = 0; i < n; ++i) {
+    comms[i] = new (std::nothrow) mano_comm{kCommMagic, devices[i], n, i, raw[i]};
+    if (!comms[i]) {
+      for (int j = 0; j < n; ++j) {
+        if (j < i) {
+          comms[j]->magic = 0;
+          delete comms[j];
+        }
+        comms[j] = nullptr;
+        r.destroy(raw[j]);
+      }
+      return fail(MANO_EINVAL, "out of host memory");
+    }
+  }
+  return MANO_OK;
+}
+
+int mano_group_start(void) {
+  mano::set_error(MANO_OK, "");
+  const Rccl& r = rccl();
+  if (!r.ok) return fail(MANO_ECOMM, "%s", r.why.c_str());
+  ncclResult_t res = r.group_start();
+  if (res != ncclSuccess) return rccl_fail(r, res, "ncclGroupStart");
+  return MANO_OK;
+}
+
+int mano_group_end(void) {
+  mano::set_error(MANO_OK, "");
+  const Rccl& r = rccl();
+  if (!r.ok) return fail(MANO_ECOMM, "%s", r.why.c_str());
+  ncclResult_t res = r.group_end();
+  if (res != ncclSuccess) return rccl_fail(r, res, "ncclGroupEnd");
   return MANO_OK;
 }
 

@@ -23,7 +23,8 @@ struct DeviceModel {
   float* pca_basis;     // [45][45]
   float* pca_mean;      // [45]
   float* zeros;         // [64] zero vector (stand-in operand for an absent trans)
-  int32_t* status;      // device status word: MANO_DEVICE_* bits raised by kernels
+  int32_t* status;      // status flags [kStatusFlags] (device address of pinned host memory):
+                        // flag b is set to 1 by a kernel raising MANO_DEVICE_* bit 1 << b
   float* basis16;       // [n_groups16][3][kTile16Floats]
   float* wfrag16;       // [n_groups16][kWFrag16Floats]
   float* basis16v;      // [kAlignVariants][n_groups16][3][kTile16Floats] sector-aligned variants,
@@ -41,6 +42,8 @@ struct DeviceModel {
   int32_t n_groups16;   // ceil(V / 16) groups of the 16x16 fused kernel (last one shifted)
   int32_t n_cu;         // compute units of the device (sizes the persistent grids)
 };
+
+constexpr int kStatusFlags = 16;  // one int32 per MANO_DEVICE_* bit (64 B)
 
 // Workspace carving (all offsets 256-B aligned).
 struct Workspace {

@@ -475,10 +475,14 @@ __device__ __forceinline__ unsigned lds_addr(const int* p) {
   return unsigned(reinterpret_cast<uintptr_t>((lds_ptr)p));  // generic -> LDS address (32 bit)
 }
 // Bounded: false after kPairPollLimit polls (2^20: tens of ms), and the
-// caller then stops -- a lost hand-over never hangs the kernel; it raises
-// MANO_DEVICE_SKIN_HANDOFF_TIMEOUT in the model's device status word
-// (mano_model_device_status), and the memory wave drops the stores of every
-// unit it could not confirm as skinned, so no un-skinned row reaches verts.
+// caller then stops -- a lost hand-over never hangs the kernel (every wave
+// reaches its exit); it raises MANO_DEVICE_SKIN_HANDOFF_TIMEOUT among the
+// model's status flags, and the memory wave drops the stores of every unit
+// it could not confirm as skinned, so no un-skinned row reaches verts.  The
+// waves of a workgroup are co-resident, so the bound is reached only by a
+// broken hand-over protocol (the diagnostic 1-poll build forces it); the
+// host then sees it: every later launch on the model returns MANO_EDEVICE
+// until mano_model_device_status clears the flag (include/mano_hip.h).
 #ifndef MANO_PAIR_POLL_LIMIT
 #define MANO_PAIR_POLL_LIMIT (1 << 20)  // diagnostic builds: tiny limits force the timeout path
 #endif
@@ -500,10 +504,15 @@ __device__ __forceinline__ bool pair_wait_ge(const int* flag, int target) {
   }
   return false;
 }
-// A hand-over wait gave up: one lane ORs the bit into the device status word
-// (a vector global atomic; read back by mano_model_device_status).
-__device__ __forceinline__ void raise_status(int* status, int bit) {
-  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or(status, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// A hand-over wait gave up: one lane sets the bit's flag among the model's
+// status flags -- pinned host memory mapped into the device, one word per
+// MANO_DEVICE_* bit, so raising it is a plain vector store at system scope
+// (no read-modify-write across the host link).  The host reads and clears
+// the flags (mano_model_device_status), and every later launch on the model
+// fails with MANO_EDEVICE until then.
+__device__ __forceinline__ void raise_status(int* flags, int bit) {
+  if ((threadIdx.x & 63) == 0)
+    __hip_atomic_store(flags + __builtin_ctz(unsigned(bit)), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ void pair_signal(int* flag, int value) {
   // the slot's LDS writes have landed before the counter moves

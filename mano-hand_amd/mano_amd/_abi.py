@@ -14,14 +14,16 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmano_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "mano_hip.h")
 
-MANO_OK, MANO_EINVAL, MANO_EHIP, MANO_ESMALL, MANO_ESTATE, MANO_ECOMM = 0, -1, -2, -3, -4, -5
+MANO_OK, MANO_EINVAL, MANO_EHIP, MANO_ESMALL, MANO_ESTATE, MANO_ECOMM, MANO_EDEVICE = 0, -1, -2, -3, -4, -5, -6
 MANO_MEMCPY_HOST_TO_DEVICE, MANO_MEMCPY_DEVICE_TO_HOST, MANO_MEMCPY_DEVICE_TO_DEVICE = 1, 2, 3
 MANO_COMM_ID_BYTES = 128
 MANO_PRECISION_FP32, MANO_PRECISION_F16X3 = 0, 1
 MANO_DEVICE_SKIN_HANDOFF_TIMEOUT = 1
+MANO_STATUS_CLEAR, MANO_STATUS_NO_WAIT = 1, 2
+ABI_VERSION = 6
 PRECISIONS = {"fp32": MANO_PRECISION_FP32, "f16x3": MANO_PRECISION_F16X3}
-_CODE_NAMES = {MANO_EINVAL: "MANO_EINVAL", MANO_EHIP: "MANO_EHIP",
-               MANO_ESMALL: "MANO_ESMALL", MANO_ESTATE: "MANO_ESTATE"}
+_CODE_NAMES = {MANO_EINVAL: "MANO_EINVAL", MANO_EHIP: "MANO_EHIP", MANO_ESMALL: "MANO_ESMALL",
+               MANO_ESTATE: "MANO_ESTATE", MANO_ECOMM: "MANO_ECOMM", MANO_EDEVICE: "MANO_EDEVICE"}
 
 
 class MissingExtensionError(RuntimeError):
@@ -34,13 +36,16 @@ class ManoError(RuntimeError):
         self.code = code
 
 
-class DeviceStatusError(RuntimeError):
-    """A kernel raised a MANO_DEVICE_* bit: some launch's outputs are not valid."""
+class DeviceStatusError(ManoError):
+    """A kernel raised a MANO_DEVICE_* bit: some launch's outputs are not
+    valid.  Raised by a wrapper that read the status (`status` = the bits), and
+    by any launching call while the bit is still set (MANO_EDEVICE)."""
 
-    def __init__(self, status):
+    def __init__(self, status, message=None):
         names = [n for n, b in (("MANO_DEVICE_SKIN_HANDOFF_TIMEOUT", MANO_DEVICE_SKIN_HANDOFF_TIMEOUT),)
                  if status & b]
-        super().__init__(f"device status 0x{status:x} ({', '.join(names) or 'unknown bits'})")
+        super().__init__(MANO_EDEVICE, message or
+                         f"device status 0x{status:x} ({', '.join(names) or 'unknown bits'})")
         self.status = status
 
 
@@ -87,6 +92,9 @@ SIGNATURES = {
                                              ctypes.c_float, ctypes.c_float, _p, _p, _p, _p]),
     "mano_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "mano_comm_create": (ctypes.c_int, [ctypes.c_int, _i32, _i32, ctypes.c_char_p, ctypes.POINTER(_p)]),
+    "mano_comm_create_all": (ctypes.c_int, [_i32, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(_p)]),
+    "mano_group_start": (ctypes.c_int, []),
+    "mano_group_end": (ctypes.c_int, []),
     "mano_comm_destroy": (ctypes.c_int, [_p]),
     "mano_gather": (ctypes.c_int, [_p, _p, ctypes.c_size_t, _p, ctypes.POINTER(ctypes.c_size_t), _i32, _p]),
     "mano_allgather": (ctypes.c_int, [_p, _p, ctypes.c_size_t, _p, _p]),
@@ -128,7 +136,11 @@ def lib() -> ctypes.CDLL:
 def check(rc: int) -> None:
     if rc != MANO_OK:
         msg = lib().mano_last_error()
-        raise ManoError(rc, msg.decode() if msg else "")
+        msg = msg.decode() if msg else ""
+        if rc == MANO_EDEVICE:
+            m = re.search(r"device status 0x([0-9a-f]+)", msg)
+            raise DeviceStatusError(int(m.group(1), 16) if m else 0, msg)
+        raise ManoError(rc, msg)
 
 
 def last_error() -> str:

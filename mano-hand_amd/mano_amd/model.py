@@ -97,18 +97,33 @@ class ManoHip:
         self.precision = precision
 
     # ------------------------------------------------------------------ utils
-    def device_status(self, clear: bool = True) -> int:
-        """The model's device status word (include/mano_hip.h
+    def device_status(self, clear: bool = True, wait: bool = True) -> int:
+        """The model's device status (include/mano_hip.h
         mano_model_device_status): 0, or MANO_DEVICE_* bits raised by a launch
-        whose outputs are not valid.  Waits for the device first."""
+        whose outputs are not valid.  `wait`: for every launch on the device
+        first; `clear`: reset the bits (until then every launching call on
+        the model raises DeviceStatusError, MANO_EDEVICE)."""
         st = ctypes.c_int32()
-        _abi.check(_abi.lib().mano_model_device_status(self._h, ctypes.byref(st), int(clear)))
+        flags = (_abi.MANO_STATUS_CLEAR if clear else 0) | (0 if wait else _abi.MANO_STATUS_NO_WAIT)
+        _abi.check(_abi.lib().mano_model_device_status(self._h, ctypes.byref(st), flags))
         return st.value
 
     def check_device(self) -> None:
         """Raise DeviceStatusError if any launch since the last check raised a
         MANO_DEVICE_* bit (the bits are cleared)."""
         st = self.device_status(clear=True)
+        if st:
+            raise _abi.DeviceStatusError(st)
+
+    def synchronize(self, stream=None) -> None:
+        """Wait for `stream` (default: the device's current stream), then raise
+        DeviceStatusError if a launch raised a MANO_DEVICE_* bit -- the point
+        at which the asynchronous stage calls' outputs are known valid.  The
+        bits stay set (later launches keep failing) until check_device() or
+        device_status(clear=True)."""
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        s.synchronize()
+        st = self.device_status(clear=False, wait=False)
         if st:
             raise _abi.DeviceStatusError(st)
 
@@ -332,6 +347,10 @@ class ManoHip:
                                                _stream_handle(self.device, stream)))
 
     def stage_skin(self, n: int, verts: torch.Tensor, rest_verts=None, trans=None, stream=None):
+        """Standalone LBS (mano_stage_skin).  Asynchronous: a lost hand-over
+        inside the kernel (MANO_DEVICE_SKIN_HANDOFF_TIMEOUT) surfaces at
+        `synchronize()` and makes every later launch on this model raise
+        DeviceStatusError until `check_device()` clears it."""
         ws, wsb = self._ws_args(n, stream=stream)
         _abi.check(_abi.lib().mano_stage_skin(self._h, n, _ptr(rest_verts), _ptr(trans),
                                               _ptr(verts), ws, wsb,

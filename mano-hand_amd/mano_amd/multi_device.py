@@ -1,0 +1,229 @@
+"""One process, one host thread, n GPUs: the single-process multi-device forward.
+
+The reference is a single process whose batch is a Python loop over hands
+(`data_explore.py:12-15` calling `mano_np.py:48-115` per hand); hands are
+independent, so this host layer splits a batch into contiguous shards
+(`distributed.shard_range`), runs each shard's forward on its own GPU and
+stream -- every launch is asynchronous, so one thread keeps all devices busy
+-- and, when the caller wants every vertex on one device, assembles the
+shards on the root GPU with ONE RCCL group from the same thread
+(`mano_comm_create_all` = ncclCommInitAll over the devices, `mano_group_start`
+/ `mano_group_end` around one `mano_gather` per device: every peer sends its
+shard straight to the root over its own xGMI link; include/mano_hip.h ABI 6).
+The root's own shard is computed in place in the assembled buffers, so only
+the peers' shards move.  `gather="copy"` assembles with peer copies instead
+(hipMemcpyPeerAsync through torch), which also works when a device is listed
+twice (a 1-GPU rehearsal of the sharding).
+
+torch supplies device memory, streams and events only; every computation is a
+libmano_hip.so launch.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from . import _abi
+from .distributed import shard_range
+from .model import ManoHip
+from .model_io import N_JOINTS
+
+
+class DeviceComms:
+    """One RCCL communicator per device, made in one call by this thread
+    (mano_comm_create_all: rank i on devices[i]), and the grouped gather."""
+
+    def __init__(self, devices: Sequence[int]):
+        self.devices = [int(d) for d in devices]
+        n = len(self.devices)
+        arr = (ctypes.c_int * n)(*self.devices)
+        comms = (ctypes.c_void_p * n)()
+        _abi.check(_abi.lib().mano_comm_create_all(n, arr, comms))
+        self._c: Optional[List[ctypes.c_void_p]] = [ctypes.c_void_p(c) for c in comms]
+
+    def gather(self, pieces: Sequence[Sequence[torch.Tensor]], outs: Sequence[torch.Tensor],
+               root: int, streams: Sequence[torch.cuda.Stream]) -> None:
+        """pieces[i][k]: device i's contiguous shard of output k (rows along
+        dim 0, shard_range order); outs[k] on devices[root] receives all rows
+        of output k.  All 2 x n mano_gather calls go in one RCCL group: they
+        are issued together when the group ends, each on its device's stream."""
+        if self._c is None:
+            raise RuntimeError("communicators are closed")
+        lib = _abi.lib()
+        n = len(self.devices)
+        _abi.check(lib.mano_group_start())
+        try:
+            for k, out in enumerate(outs):
+                row = math.prod(out.shape[1:]) * out.element_size()
+                sizes = (ctypes.c_size_t * n)(*[pieces[i][k].shape[0] * row for i in range(n)])
+                for i in range(n):
+                    p = pieces[i][k]
+                    _abi.check(lib.mano_gather(
+                        self._c[i], ctypes.c_void_p(p.data_ptr()), p.shape[0] * row,
+                        ctypes.c_void_p(out.data_ptr()) if i == root else None, sizes, root,
+                        ctypes.c_void_p(streams[i].cuda_stream)))
+        finally:
+            _abi.check(lib.mano_group_end())
+
+    def close(self):
+        if self._c is not None:
+            for c in self._c:
+                _abi.check(_abi.lib().mano_comm_destroy(c))
+            self._c = None
+
+
+class ManoMultiDevice:
+    """The MANO forward over several GPUs from one host thread.
+
+    devices: GPU indices (default: every visible GPU); root: the index INTO
+    `devices` of the GPU that receives gathered outputs."""
+
+    def __init__(self, params: Dict[str, object], devices: Optional[Sequence[int]] = None,
+                 precision: str = "fp32", root: int = 0):
+        if devices is None:
+            devices = list(range(torch.cuda.device_count()))
+        self.devices = [int(d) for d in devices]
+        if not self.devices:
+            raise ValueError("no devices")
+        if not 0 <= root < len(self.devices):
+            raise ValueError(f"root {root} is not an index into devices {self.devices}")
+        self.root = root
+        self.engines = [ManoHip(params, device=d, precision=precision) for d in self.devices]
+        self.streams = [torch.cuda.Stream(device=d) for d in self.devices]
+        self.n_verts = self.engines[0].n_verts
+        self._comms: Optional[DeviceComms] = None
+
+    @property
+    def root_device(self) -> torch.device:
+        return torch.device("cuda", self.devices[self.root])
+
+    def shard_ranges(self, n_total: int):
+        n = len(self.devices)
+        return [shard_range(n_total, r, n) for r in range(n)]
+
+    def comms(self) -> DeviceComms:
+        """The RCCL communicators (made on first use)."""
+        if self._comms is None:
+            self._comms = DeviceComms(self.devices)
+        return self._comms
+
+    # ---------------------------------------------------------------- forward
+    def _alloc_outputs(self, n_total, joints, gather):
+        """Per device: the (verts, joints) its forward writes.  With a gather,
+        the root's rows of the assembled buffers (allocated on the root's
+        stream) are its outputs, so its shard never moves."""
+        V = self.n_verts
+        ranges = self.shard_ranges(n_total)
+        assembled = None
+        if gather:
+            rd, rs = self.root_device, self.streams[self.root]
+            with torch.cuda.device(rd), torch.cuda.stream(rs):
+                assembled = {"verts": torch.empty((n_total, V, 3), device=rd)}
+                if joints:
+                    assembled["joints"] = torch.empty((n_total, N_JOINTS, 3), device=rd)
+        per = []
+        for i, (d, s) in enumerate(zip(self.devices, self.streams)):
+            a, b = ranges[i]
+            if gather and i == self.root:
+                per.append({k: t[a:b] for k, t in assembled.items()})
+                continue
+            with torch.cuda.device(d), torch.cuda.stream(s):
+                o = {"verts": torch.empty((b - a, V, 3), device=torch.device("cuda", d))}
+                if joints:
+                    o["joints"] = torch.empty((b - a, N_JOINTS, 3), device=torch.device("cuda", d))
+            per.append(o)
+        return ranges, per, assembled
+
+    def _finish(self, ranges, per, assembled, joints, gather):
+        keys = ["verts"] + (["joints"] if joints else [])
+        if gather == "rccl":
+            self.comms().gather([[per[i][k] for k in keys] for i in range(len(self.devices))],
+                                [assembled[k] for k in keys], self.root, self.streams)
+        elif gather == "copy":
+            rd, rs = self.root_device, self.streams[self.root]
+            for i, s in enumerate(self.streams):
+                if i == self.root:
+                    continue
+                a, b = ranges[i]
+                if b == a:
+                    continue
+                rs.wait_stream(s)            # the peer's shard is written
+                with torch.cuda.device(rd), torch.cuda.stream(rs):
+                    for k in keys:
+                        assembled[k][a:b].copy_(per[i][k], non_blocking=True)
+                # the peer's buffers are read on the root's stream: their
+                # memory returns to the peer's pool only after that copy
+                for k in keys:
+                    per[i][k].record_stream(rs)
+        if gather:
+            # the caller's current stream on the root orders after the gather
+            # (and, for RCCL, the peers' sends ran on their own streams, which
+            # the root's receive completes with)
+            torch.cuda.current_stream(self.root_device).wait_stream(self.streams[self.root])
+            return assembled
+        for d, s in zip(self.devices, self.streams):
+            torch.cuda.current_stream(torch.device("cuda", d)).wait_stream(s)
+        return per
+
+    def forward(self, betas: torch.Tensor, pose: torch.Tensor, trans: Optional[torch.Tensor] = None, *,
+                joints: bool = True, gather="rccl"):
+        """Batched forward of (B,10) betas and (B,16,3) poses (and (B,3)
+        trans), on any one device or the host, split over the devices.
+
+        gather "rccl" / "copy": returns {"verts": (B,V,3), "joints": (B,16,3)}
+        on the root device; False: a list of per-device dicts holding rows
+        shard_range(B, i, n) of the batch."""
+        if gather not in ("rccl", "copy", False, None):
+            raise ValueError(f"gather must be 'rccl', 'copy' or False, got {gather!r}")
+        gather = gather or False
+        B = pose.shape[0]
+        pose = pose.reshape(B, N_JOINTS, 3)
+        ranges, per, assembled = self._alloc_outputs(B, joints, gather)
+        src_stream = torch.cuda.current_stream(pose.device) if pose.is_cuda else None
+        for i, (eng, d, s) in enumerate(zip(self.engines, self.devices, self.streams)):
+            a, b = ranges[i]
+            if b == a:
+                continue
+            dev = torch.device("cuda", d)
+            if src_stream is not None:
+                s.wait_stream(src_stream)    # the inputs are written
+            with torch.cuda.device(dev), torch.cuda.stream(s):
+                take = lambda t: None if t is None else t[a:b].to(dev, non_blocking=True).contiguous()  # noqa: E731
+                bt = betas if betas.dim() == 1 else betas[a:b]
+                bt = bt.to(dev, non_blocking=True).contiguous()
+                eng.forward(bt, take(pose), take(trans), joints=joints, out=per[i], stream=s)
+        return self._finish(ranges, per, assembled, joints, gather)
+
+    def forward_synthetic(self, seed: int, n_total: int, *, trans: bool = False, joints: bool = True,
+                          gather="rccl"):
+        """The forward of global hands 0..n_total-1 of the counter-based
+        synthetic batch (mano_synthetic_inputs): each device generates its own
+        shard's inputs by global index, so no input crosses a link."""
+        if gather not in ("rccl", "copy", False, None):
+            raise ValueError(f"gather must be 'rccl', 'copy' or False, got {gather!r}")
+        gather = gather or False
+        ranges, per, assembled = self._alloc_outputs(n_total, joints, gather)
+        for i, (eng, s) in enumerate(zip(self.engines, self.streams)):
+            a, b = ranges[i]
+            if b == a:
+                continue
+            inp = eng.synthetic_inputs(seed, a, b - a, trans=trans, stream=s)  # allocated on s
+            eng.forward(inp["betas"], inp["pose"], inp.get("trans"), joints=joints, out=per[i], stream=s)
+        return self._finish(ranges, per, assembled, joints, gather)
+
+    def synchronize(self) -> None:
+        """Wait for every device's stream; raise DeviceStatusError if a launch
+        on any device raised a MANO_DEVICE_* bit."""
+        for eng, s in zip(self.engines, self.streams):
+            eng.synchronize(s)
+
+    def close(self) -> None:
+        if self._comms is not None:
+            self._comms.close()
+            self._comms = None
+        for e in self.engines:
+            e.close()
+        self.engines = []

@@ -17,7 +17,7 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, n), n
         assert n in _abi.SIGNATURES, f"{n} declared in the header but not bound"
     assert set(_abi.SIGNATURES) == set(names)
-    assert lib.mano_abi_version() == 5
+    assert lib.mano_abi_version() == _abi.ABI_VERSION == 6
 
 
 @pytest.mark.parametrize("cc,lang", [("g++", "c++"), ("gcc", "c")])
@@ -129,6 +129,33 @@ def test_device_status_argument_checks():
     assert st.value == 7
 
 
+def test_edevice_maps_to_device_status_error():
+    """MANO_EDEVICE (a launch refused while a status bit is set) raises the
+    DeviceStatusError the wrappers document, with the bits from the message."""
+    import unittest.mock as um
+    fake = um.MagicMock()
+    fake.mano_last_error.return_value = b"device status 0x1: an earlier launch ..."
+    with um.patch.object(_abi, "lib", return_value=fake):
+        with pytest.raises(_abi.DeviceStatusError) as ei:
+            _abi.check(_abi.MANO_EDEVICE)
+    assert ei.value.code == _abi.MANO_EDEVICE and ei.value.status == 1
+    assert isinstance(ei.value, _abi.ManoError)
+
+
+def test_single_process_comm_argument_checks():
+    """ABI 6's one-thread-many-devices communicators refuse bad arguments
+    before touching RCCL or a GPU."""
+    lib = _abi.lib()
+    comms = (ctypes.c_void_p * 2)()
+    devs = (ctypes.c_int * 2)(0, 0)
+    assert lib.mano_comm_create_all(0, devs, comms) == _abi.MANO_EINVAL
+    assert lib.mano_comm_create_all(2, None, comms) == _abi.MANO_EINVAL
+    assert lib.mano_comm_create_all(2, devs, None) == _abi.MANO_EINVAL
+    neg = (ctypes.c_int * 1)(-1)
+    assert lib.mano_comm_create_all(1, neg, comms) in (_abi.MANO_EINVAL, _abi.MANO_EHIP)
+    assert comms[0] is None
+
+
 def test_host_block_mapped_is_false_for_pageable_memory():
     """The drop-in's zero-copy guard (hipPointerGetAttributes through the
     runtime libmano_hip.so links) answers False for ordinary pageable host
@@ -158,7 +185,8 @@ def test_ffi_binding_signatures_match_header():
     code = ("import sys; sys.path.insert(0, %r); import mano_hip_ffi as f; "
             "print({n: len(getattr(f._lib, n).argtypes) for n in ('mano_model_create', 'mano_forward', "
             "'mano_alloc', 'mano_free', 'mano_memcpy', 'mano_host_alloc', 'mano_host_free', 'mano_synchronize', "
-            "'mano_forward_workspace_bytes', 'mano_model_destroy')}); print('torch' in sys.modules)"
+            "'mano_forward_workspace_bytes', 'mano_model_destroy', 'mano_model_device_status')}); "
+            "print('torch' in sys.modules)"
             % os.path.join(REPO, "integration"))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr

@@ -1,0 +1,143 @@
+"""The single-process multi-GPU path (mano_amd.multi_device, include/mano_hip.h
+ABI 6: mano_comm_create_all + mano_group_start / mano_group_end).
+
+One host thread drives every device: shards of one batch run on their own
+GPUs and streams, and the assembled outputs on the root equal the
+single-handle forward of the whole batch bit for bit (hands are independent,
+mano_np.py:79-115; the batch is the reference's single-process loop,
+data_explore.py:12-15).  On the 1-GPU pool the RCCL form runs at n = 1
+(ncclCommInitAll over one device) and the sharding / stream / assembly logic
+with one GPU listed several times (peer-copy assembly); the n = 2 RCCL case
+runs wherever 2 GPUs are visible."""
+import ctypes
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def _reference(params, seed, n, trans):
+    from mano_amd import ManoHip
+    m = ManoHip(params, device=0)
+    inp = m.synthetic_inputs(seed, 0, n, trans=trans)
+    out = m.forward(inp["betas"], inp["pose"], inp.get("trans"), joints=True)
+    torch.cuda.synchronize()
+    res = {k: v.cpu() for k, v in out.items()}, {k: v.cpu() for k, v in inp.items()}
+    m.close()
+    return res
+
+
+def test_one_device_rccl_group_gather_bit_exact(params):
+    """n = 1: mano_comm_create_all over device 0, the grouped gather (the
+    root's shard in place), bit-exact against the single-handle forward --
+    from synthetic inputs generated per device and from caller inputs."""
+    from mano_amd import ManoMultiDevice
+    n, seed = 1000, 1004
+    ref, inp = _reference(params, seed, n, trans=True)
+    md = ManoMultiDevice(params, devices=[0])
+    try:
+        out = md.forward_synthetic(seed, n, trans=True, gather="rccl")
+        torch.cuda.synchronize()
+        assert out["verts"].device == torch.device("cuda", 0)
+        assert torch.equal(out["verts"].cpu(), ref["verts"]) and torch.equal(out["joints"].cpu(), ref["joints"])
+        d = torch.device("cuda", 0)
+        out2 = md.forward(inp["betas"].to(d), inp["pose"].to(d), inp["trans"].to(d), gather="rccl")
+        md.synchronize()
+        assert torch.equal(out2["verts"].cpu(), ref["verts"]) and torch.equal(out2["joints"].cpu(), ref["joints"])
+    finally:
+        md.close()
+
+
+def test_abi_group_gather_not_in_place():
+    """The ABI directly: one communicator from mano_comm_create_all, a
+    mano_gather between mano_group_start / mano_group_end whose send is NOT
+    the root's slot (the root copies its shard), bytes equal."""
+    from mano_amd import _abi
+    lib = _abi.lib()
+    comms = (ctypes.c_void_p * 1)()
+    _abi.check(lib.mano_comm_create_all(1, (ctypes.c_int * 1)(0), comms))
+    try:
+        src = torch.arange(3 * 1024, dtype=torch.float32, device="cuda:0")
+        dst = torch.zeros(3 * 1024 + 64, dtype=torch.float32, device="cuda:0")
+        s = torch.cuda.current_stream(0)
+        sizes = (ctypes.c_size_t * 1)(src.numel() * 4)
+        _abi.check(lib.mano_group_start())
+        _abi.check(lib.mano_gather(ctypes.c_void_p(comms[0]), ctypes.c_void_p(src.data_ptr()), src.numel() * 4,
+                                   ctypes.c_void_p(dst.data_ptr()), sizes, 0, ctypes.c_void_p(s.cuda_stream)))
+        _abi.check(lib.mano_group_end())
+        torch.cuda.synchronize()
+        assert torch.equal(dst[:src.numel()], src) and not dst[src.numel():].any()
+    finally:
+        _abi.check(lib.mano_comm_destroy(ctypes.c_void_p(comms[0])))
+
+
+def test_duplicate_device_refused_by_rccl_form():
+    from mano_amd import DeviceComms, _abi
+    with pytest.raises(_abi.ManoError) as ei:
+        DeviceComms([0, 0])
+    assert ei.value.code == _abi.MANO_EINVAL and "twice" in str(ei.value)
+
+
+@pytest.mark.parametrize("gather", ["copy", False])
+def test_shards_over_one_gpu_listed_three_times(params, gather):
+    """The sharding, per-device streams and assembly with 3 engines (one GPU
+    listed three times): a ragged 1,003-hand batch (335 + 334 + 334) equals
+    the single-handle forward bit for bit, assembled by peer copies or as
+    per-device shards."""
+    from mano_amd import ManoMultiDevice
+    from mano_amd.distributed import shard_range
+    n, seed = 1003, 1002
+    ref, _ = _reference(params, seed, n, trans=False)
+    md = ManoMultiDevice(params, devices=[0, 0, 0], root=1)
+    try:
+        out = md.forward_synthetic(seed, n, gather=gather)
+        torch.cuda.synchronize()
+        if gather:
+            assert torch.equal(out["verts"].cpu(), ref["verts"]) and torch.equal(out["joints"].cpu(), ref["joints"])
+        else:
+            assert len(out) == 3
+            for i, o in enumerate(out):
+                a, b = shard_range(n, i, 3)
+                assert torch.equal(o["verts"].cpu(), ref["verts"][a:b])
+                assert torch.equal(o["joints"].cpu(), ref["joints"][a:b])
+    finally:
+        md.close()
+
+
+def test_host_inputs_and_shared_betas(params):
+    """Caller inputs on the host with one shared beta row, split over 2
+    engines: equal to the single-handle forward of the same inputs."""
+    from mano_amd import ManoHip, ManoMultiDevice
+    rng = np.random.default_rng(5)
+    n = 77
+    betas = torch.tensor(rng.normal(0, 1, 10), dtype=torch.float32)
+    pose = torch.tensor(rng.normal(0, 0.5, (n, 16, 3)), dtype=torch.float32)
+    m = ManoHip(params, device=0)
+    ref = m.forward(betas.cuda(), pose.cuda(), joints=True)
+    torch.cuda.synchronize()
+    md = ManoMultiDevice(params, devices=[0, 0])
+    try:
+        out = md.forward(betas, pose, gather="copy")
+        md.synchronize()
+        assert torch.equal(out["verts"], ref["verts"]) and torch.equal(out["joints"], ref["joints"])
+    finally:
+        md.close()
+        m.close()
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="the RCCL group gather needs 2 GPUs")
+def test_two_devices_rccl_group_gather(params):
+    """n = 2 for real: one thread, two GPUs, one RCCL group; GPU 0's
+    assembled outputs of a ragged batch equal the single-handle forward."""
+    from mano_amd import ManoMultiDevice
+    n, seed = 1003, 1004
+    ref, _ = _reference(params, seed, n, trans=True)
+    md = ManoMultiDevice(params, devices=[0, 1])
+    try:
+        out = md.forward_synthetic(seed, n, trans=True, gather="rccl")
+        md.synchronize()
+        assert torch.equal(out["verts"].cpu(), ref["verts"]) and torch.equal(out["joints"].cpu(), ref["joints"])
+    finally:
+        md.close()
