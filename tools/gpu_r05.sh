@@ -10,11 +10,11 @@ export TMPDIR=/tmp
 step() {  # name timeout cmd...
   local name=$1 t=$2; shift 2
   echo "=== $name: $*" | tee -a $OUT/steps.log
-  local t0=$(date +%s.%N)
+  local t0=$(date +%s%N)
   timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
-  local t1=$(date +%s.%N)
-  echo "=== $name rc=$rc wall_s=$(echo "$t1 - $t0" | bc)" | tee -a $OUT/steps.log
+  local t1=$(date +%s%N)
+  echo "=== $name rc=$rc wall_ms=$(( (t1 - t0) / 1000000 ))" | tee -a $OUT/steps.log
   tail -3 "$OUT/$name.log" | cut -c1-600
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after rc=$rc"; exit $rc; fi
   if [ $rc -eq 1 ] && [ "${STOP_ON_FAIL:-1}" = 1 ]; then echo "stopping after rc=1"; exit 1; fi
