@@ -61,13 +61,12 @@ extern "C" {
  *         v_mfma_f32_16x16x32_f16 (16/3 x the fp32 MFMA rate).  Same error
  *         order as FP32 vs the float64 reference (~1e-7 m); needs |beta| and
  *         the pose features within f16 range and skinning transforms < 1000.
- *         Known, guarded, not understood: built with packed fp32 VALU
- *         (v_pk_fma_f32 with an SGPR-pair operand, which the SLP vectorizer
- *         makes of the LBS unscale), the rest_verts instantiations returned
- *         wrong x coordinates under memory load; no hardware rule explaining it
- *         is known.  Correctness rests on the build flag
- *         -fno-slp-vectorize and on ISA checks that no packed fp32 op exists in
- *         the library (tests/test_codegen.py, tests/test_gpu_codegen.py). */
+ *         Used for verts-only forwards and for mano_stage_skin; a
+ *         mano_forward / mano_forward_pca / mano_stage_blend_skin call that
+ *         requests rest_verts runs the FP32 kernel (the f16x3 kernel with a
+ *         rest_verts output is not built: its vectorized form miscomputed
+ *         under load for a reason never explained).
+ *         mano_stage_blend is always FP32. */
 #define MANO_PRECISION_FP32 0
 #define MANO_PRECISION_F16X3 1
 

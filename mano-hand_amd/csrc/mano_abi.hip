@@ -404,12 +404,16 @@ int mano_stage_blend_skin(const mano_model* m, int64_t n, float* rest_verts, con
   if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
   const mano::Workspace w = mano::workspace_layout(m->dm, n);
   char* base = static_cast<char*>(ws);
-  auto launch = m->dm.precision == MANO_PRECISION_F16X3 ? mano::launch_blend_skin_h3
-                                                          : mano::launch_blend_skin;
-  hipError_t e = launch(
-      m->dm, n, reinterpret_cast<const float*>(base + w.features_off),
-      reinterpret_cast<const float*>(base + w.transforms_off), trans, verts, rest_verts,
-      static_cast<hipStream_t>(stream));
+  const float* feats = reinterpret_cast<const float*>(base + w.features_off);
+  const float* frames = reinterpret_cast<const float*>(base + w.transforms_off);
+  // F16X3 covers verts-only calls: the product has no f16x3 kernel that also
+  // writes rest_verts (mano_kernels_h3.hip header), so such a call runs the
+  // exact-fp32 kernel -- same outputs to ~1e-7 m, more exact.
+  hipError_t e = m->dm.precision == MANO_PRECISION_F16X3 && !rest_verts
+                     ? mano::launch_blend_skin_h3(m->dm, n, feats, frames, trans, verts,
+                                                  static_cast<hipStream_t>(stream))
+                     : mano::launch_blend_skin(m->dm, n, feats, frames, trans, verts, rest_verts,
+                                               static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "blend_skin launch");
   return MANO_OK;
 }

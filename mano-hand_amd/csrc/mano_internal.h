@@ -94,10 +94,10 @@ hipError_t launch_skin_quad(const DeviceModel& m, int64_t n, const float* transf
                             const float* vposed, const float* trans, float* verts,
                             hipStream_t stream, bool h3 = false);
 // f16x3 mode (mano_kernels_h3.hip): same operands and outputs as
-// launch_blend_skin / launch_skin.
+// launch_blend_skin (verts only: no v_posed output) / launch_skin.
 hipError_t launch_blend_skin_h3(const DeviceModel& m, int64_t n, const float* features,
                                 const float* transforms, const float* trans, float* verts,
-                                float* vposed, hipStream_t stream);
+                                hipStream_t stream);
 hipError_t launch_skin_h3(const DeviceModel& m, int64_t n, const float* transforms,
                           const float* vposed, const float* trans, float* verts,
                           hipStream_t stream);

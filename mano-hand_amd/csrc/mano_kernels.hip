@@ -80,6 +80,9 @@ __device__ __forceinline__ f32x16 mfma_tile(const float (&a)[kKGroups * 4], cons
 #ifndef MANO_BLEND_STORE_POLICY
 #define MANO_BLEND_STORE_POLICY 1  // buffer-store cache policy bits of v_posed (1 = sc0; diagnostic builds: others)
 #endif
+#ifndef MANO_BLEND_COUNTED
+#define MANO_BLEND_COUNTED 0  // blend_kernel: 1 = counted-vmcnt barriers (diagnostic: 0.363 vs 0.359 ms with sc0 stores, 0.387 vs 0.403 nontemporal; profiles/r05/r05b_blend_ab.jsonl)
+#endif
 __device__ __forceinline__ void store_vposed_tile(float* __restrict__ vposed, const f32x16& acc,
                                                   int64_t h0, int lp, int n_valid, int col, int n_cols,
                                                   int hi) {
@@ -87,13 +90,15 @@ __device__ __forceinline__ void store_vposed_tile(float* __restrict__ vposed, co
   const int rstride = n_cols << lp;
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(vposed + h0 * n_cols, 0, ((n_valid - 1) * rstride + n_cols) * 4,
                                                     0x00020000);
-  if (col < n_cols) {
+  // Every lane issues its 16 stores (the blend kernel's counted vmcnt needs
+  // an exact per-wave count); a lane past the row end gets an offset beyond
+  // the buffer, whose store is dropped.
+  const int cbase = col < n_cols ? 4 * col : 0x7fff0000;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int hr = (r & 3) + 8 * (r >> 2) + 4 * hi;
-      const float x = acc[r];  // a scalar first: __builtin_bit_cast of a vector element reads element 0
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), rs, 4 * (hr * rstride + col), 0, MANO_BLEND_STORE_POLICY);
-    }
+  for (int r = 0; r < 16; ++r) {
+    const int hr = (r & 3) + 8 * (r >> 2) + 4 * hi;
+    const float x = acc[r];  // a scalar first: __builtin_bit_cast of a vector element reads element 0
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), rs, cbase + 4 * hr * rstride, 0, MANO_BLEND_STORE_POLICY);
   }
 }
 
@@ -149,12 +154,32 @@ __global__ __launch_bounds__(256, 2) void blend_kernel(
   // before tile t+2's LDS-DMA, so the barrier's vmcnt(0) only waits on old
   // stores and the DMA the MFMA chain has already hidden.
   f32x16 prev = {};
+#if MANO_BLEND_COUNTED
+  // Tile t+1's LDS-DMA first, then tile t-1's 16 stores: the barrier waits
+  // with vmcnt(16), so those stores stay in flight through the next tile's
+  // MFMA chain (in issue order, they must retire before the NEXT barrier's
+  // DMA does) instead of gating this one -- a store policy whose completion
+  // takes longer (nontemporal) no longer stalls every tile.
+  for (int t = 0; t < n_col_tiles; ++t) {
+    if (t + 1 < n_col_tiles) stage_basis_tile(tiles, t + 1, bs[(t + 1) & 1], wave, lane);
+    asm volatile("" ::: "memory");  // the DMA stays older than the stores (the vmcnt count)
+    __builtin_amdgcn_sched_barrier(0);
+    if (t > 0) store_vposed_tile(vposed, prev, tile.h0, lp, tile.n_valid, col_of(t - 1), n_cols, hi);
+    prev = mfma_tile(a, bs[t & 1], lane);
+    if (t == 0) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+  }
+#else
   for (int t = 0; t < n_col_tiles; ++t) {
     if (t > 0) store_vposed_tile(vposed, prev, tile.h0, lp, tile.n_valid, col_of(t - 1), n_cols, hi);
     if (t + 1 < n_col_tiles) stage_basis_tile(tiles, t + 1, bs[(t + 1) & 1], wave, lane);
     prev = mfma_tile(a, bs[t & 1], lane);
     __syncthreads();
   }
+#endif
   store_vposed_tile(vposed, prev, tile.h0, lp, tile.n_valid, col_of(n_col_tiles - 1), n_cols, hi);
 }
 

@@ -22,24 +22,21 @@
 //
 // Packed fp32 VALU (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32) is kept out of
 // these kernels: every scalar result the vectorizer could pair goes through
-// no_pack(), and the library is built with -fno-slp-vectorize.  With the
-// vectorizer on, blend_skin_h3's rest_verts instantiations returned wrong x
-// coordinates for hand rows 14-15 under load; round 2 localized it to the
-// v_pk_fma_f32 with an SGPR-pair multiplier made of the final
-// fma(o, 2^-k, trans) -- scalarizing only that multiply removes every failure
-// -- and excluded wait-state hazards, the counted vmcnt barriers, stray
-// stores and spills (tools/debug/h3_root_cause.sh).  Packed
-// fp32 beside MFMA is also the slower form on gfx950 (MI355X_MICROARCH.md).
+// no_pack(), and the library is built with -fno-slp-vectorize.  Packed fp32
+// beside MFMA is also the slower form on gfx950 (MI355X_MICROARCH.md).
 //
-// Status, plainly: the miscompute is GUARDED, NOT UNDERSTOOD.  No hardware
-// rule that would explain it is known (the instruction windows of the
-// failing and passing builds differ only in 6-7 vs 1-3 stores in flight,
-// profiles/r03_f16x3_windows.jsonl; no errata are available offline).  This
-// mode is correct because the build flag -fno-slp-vectorize and no_pack()
-// keep the instruction form out, and because tests/test_codegen.py and
-// tests/test_gpu_codegen.py fail on any packed fp32 op in the library.  It
-// stays opt-in (MANO_PRECISION_F16X3); the default fp32 path has no packed
-// fp32 either.
+// The fused kernel has NO rest_verts (v_posed output) instantiation.  Built
+// with the vectorizer on, those instantiations -- and only those -- returned
+// wrong x coordinates for hand rows 14-15 under load; round 2 localized it to
+// a v_pk_fma_f32 with an SGPR-pair multiplier (the LBS output's final
+// fma(o, 2^-k, trans)) and excluded wait-state hazards, the counted vmcnt
+// barriers, stray stores and spills, but no hardware or compiler rule that
+// explains it was found (profiles/r03_f16x3_windows.jsonl).
+// Rather than ship a kernel whose correctness rests on a guard nobody can
+// explain, the product does not build it: an F16X3 call that asks for
+// rest_verts runs the exact-fp32 blend_skin16 (mano_abi.hip), so f16x3
+// arithmetic is used for verts-only forwards.  The guards stay (no_pack,
+// -fno-slp-vectorize, the ISA scans of tests/test_codegen.py).
 #include "mano_internal.h"
 #include "mano_span.h"
 
@@ -271,6 +268,24 @@ constexpr int kH3TPW = MANO_H3_TPW;  // 16-hand tiles per wave (each B piece rea
 #define MANO_H3_BLOCKS 1
 #endif
 constexpr int kH3BlocksPerCU = MANO_H3_BLOCKS;
+#ifndef MANO_H3_RING
+#define MANO_H3_RING 2
+#endif
+// LDS slots of blend_skin_h3's basis ring (32 KB each; groups staged ahead =
+// kH3Ring - 1).  160 KB of LDS per CU holds at most 4 with one block per CU.
+constexpr int kH3Ring = MANO_H3_RING;
+static_assert(kH3Ring >= 2 && kH3Ring <= 4 && kH3Ring * 32 * 1024 * kH3BlocksPerCU <= 160 * 1024, "basis ring exceeds the LDS");
+
+// barrier_vmcnt<kBase + d * (DMA ops per group)> for d = later_dmas (a
+// runtime value: one branch per count, each an immediate s_waitcnt).
+template <int kBase>
+__device__ __forceinline__ void ring_barrier(int later_dmas) {
+  constexpr int kDma = kH3GroupPieces / kH3Waves;  // global_load_lds per wave per group
+  if (later_dmas <= 0) barrier_vmcnt<kBase>();
+  else if (later_dmas == 1) barrier_vmcnt<kBase + kDma>();
+  else barrier_vmcnt<kBase + 2 * kDma>();
+}
+
 
 // One group's 32 fragment pieces (32 KB), global -> LDS, 32 / kH3Waves per wave.
 __device__ __forceinline__ void stage_group_h3(const uint16_t* __restrict__ basis_h3, int grp,
@@ -287,8 +302,8 @@ __device__ __forceinline__ void stage_group_h3(const uint16_t* __restrict__ basi
   asm volatile("" ::: "memory");
 }
 
-// Fused blend GEMM + LBS, f16x3.  A block (kH3Waves waves, kH3TPW 16-hand
-// tiles each) owns a contiguous range of (block tile set, vertex group)
+// Fused blend GEMM + LBS, f16x3, verts only.  A block (kH3Waves waves, kH3TPW
+// 16-hand tiles each) owns a contiguous range of (block tile set, vertex group)
 // units; the group's basis + weight pieces are LDS-DMA-staged once per block,
 // one group ahead (ring of 2 x 32 KB), and every B piece a wave reads feeds its
 // kH3TPW tiles.  Each group ends with an explicit vmcnt wait: the next
@@ -296,16 +311,16 @@ __device__ __forceinline__ void stage_group_h3(const uint16_t* __restrict__ basi
 // vmcnt(kStores) covers it without waiting for the stores themselves.  Stores
 // are branch-free (rows past the batch end rewrite the last hand's identical
 // values), so their count is exact.
-template <bool kTrans, bool kVposed>
+template <bool kTrans>
 __global__ __launch_bounds__(64 * kH3Waves, kH3BlocksPerCU) void blend_skin_h3_kernel(
     const float* __restrict__ features, const float* __restrict__ transforms,
     const uint16_t* __restrict__ basis_h3, const float* __restrict__ trans,
-    float* __restrict__ verts, float* __restrict__ vposed, int64_t n, int n_verts, int n_groups,
+    float* __restrict__ verts, int64_t n, int n_verts, int n_groups,
     float p_unscale, float t_unscale, int lp, unsigned shifts, int aligned) {
   constexpr int kSlot = kH3GroupPieces * 64;                // f16x8 per slot (32 KB)
-  constexpr int kStores = (MANO_H3_ABLATE & 2) ? 0 : (kVposed ? 8 : 4) * kH3TPW;  // global_store_dwordx3 per group
+  constexpr int kStores = (MANO_H3_ABLATE & 2) ? 0 : 4 * kH3TPW;  // global_store_dwordx3 per group
   constexpr int kTiles = kH3Waves * kH3TPW;                 // hand tiles per block unit
-  __shared__ f16x8 ring[2 * kSlot];
+  __shared__ f16x8 ring[kH3Ring * kSlot];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   static_assert(kTiles == 8, "residue-class sets of 8 16-hand tiles (mano_layout.h, lq = 7)");
   const int vstride = 3 * n_verts;
@@ -327,17 +342,19 @@ __global__ __launch_bounds__(64 * kH3Waves, kH3BlocksPerCU) void blend_skin_h3_k
     const int q = lane >> 4;
     const int col = lane & 15;
 
-    const AlignedTile tile = aligned_tile(n, lp, set, wave, 7, 4);
-    const int shift = aligned ? int((shifts >> (4 * tile.cls)) & 15u) : 0;
+    // the set's tiles share one residue class, so one basis variant
+    const int shift = aligned ? int((shifts >> (4 * aligned_tile(n, lp, set, wave * kH3TPW, 7, 4).cls)) & 15u) : 0;
     const uint16_t* bvar = basis_h3 + (aligned ? int64_t(shift) * n_groups * kH3GroupHalves : 0);
-    stage_group_h3(bvar, g0, ring, wave, lane);
+#pragma unroll
+    for (int i = 0; i < kH3Ring - 1; ++i)
+      if (g0 + i < g1) stage_group_h3(bvar, g0 + i, ring + i * kSlot, wave, lane);
     f16x8 xh[kH3TPW][kH3Steps], xl[kH3TPW][kH3Steps], F[kH3TPW][12];
     float tr[kH3TPW][4][3] = {};
     unsigned roff[kH3TPW][4];  // D rows (hands 4q + r) of each tile, clamped to the batch
     float* vtile[kH3TPW];
-    float* ptile[kH3TPW];
 #pragma unroll
     for (int t = 0; t < kH3TPW; ++t) {
+      const AlignedTile tile = aligned_tile(n, lp, set, wave * kH3TPW + t, 7, 4);
       // A tile past the batch end recomputes the set's last tile (identical
       // values).  The tile's rows are hands h0 + (i << lp), i <= rmax.
       const int64_t h0 = tile.h0;
@@ -357,15 +374,17 @@ __global__ __launch_bounds__(64 * kH3Waves, kH3BlocksPerCU) void blend_skin_h3_k
         }
       }
       vtile[t] = verts + h0 * int64_t(vstride);
-      ptile[t] = kVposed ? vposed + h0 * int64_t(vstride) : nullptr;
     }
-    // The first group's pieces and every prologue load have landed.
+    // The first kH3Ring - 1 groups' pieces and every prologue load have landed.
     barrier_vmcnt<0>();
 
-    for (int grp = g0, slot = 0; grp < g1; ++grp, slot ^= 1) {
-      if (!(MANO_H3_ABLATE & 8) && grp + 1 < g1) {
+    for (int grp = g0, slot = 0; grp < g1; ++grp, slot = slot + 1 < kH3Ring ? slot + 1 : 0) {
+      // group grp + kH3Ring - 1 into the slot group grp - 1 left (every wave
+      // passed the barrier that ended group grp - 1)
+      if (!(MANO_H3_ABLATE & 8) && grp + kH3Ring - 1 < g1) {
         if constexpr (MANO_H3_DMA_PRIO != 0) __builtin_amdgcn_s_setprio(MANO_H3_DMA_PRIO);
-        stage_group_h3(bvar, grp + 1, ring + (slot ^ 1) * kSlot, wave, lane);
+        const int ahead = slot + kH3Ring - 1 < kH3Ring ? slot + kH3Ring - 1 : slot - 1;
+        stage_group_h3(bvar, grp + kH3Ring - 1, ring + ahead * kSlot, wave, lane);
         if constexpr (MANO_H3_DMA_PRIO != 0) __builtin_amdgcn_s_setprio(0);
       }
       const f16x8* L = ring + slot * kSlot + lane;
@@ -434,12 +453,15 @@ __global__ __launch_bounds__(64 * kH3Waves, kH3BlocksPerCU) void blend_skin_h3_k
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           store_out_h3(vtile[t] + (roff[t][r] + unsigned(voff)), f32x3{out[0][r], out[1][r], out[2][r]});
-          if constexpr (kVposed) store_out_h3(ptile[t] + (roff[t][r] + unsigned(voff)), f32x3{p[t][0][r], p[t][1][r], p[t][2][r]});
         }
       }
       // Group grp + 1 has landed in LDS (every wave's pieces) and every wave
-      // is done reading this slot, which the next iteration re-stages.
-      barrier_vmcnt<kStores>();
+      // is done reading this slot, which the next iteration re-stages.  The
+      // ops younger than group grp + 1's DMA (issued kH3Ring - 2 iterations
+      // ago, or in the prologue) are the kH3Ring - 1 groups' stores and the
+      // DMAs of groups grp + 2 .. grp + kH3Ring - 1 that exist in the range.
+      const int later_dmas = min(kH3Ring - 2, max(0, g1 - grp - 2));
+      ring_barrier<(kH3Ring - 1) * kStores>(later_dmas);
     }
   }
 }
@@ -543,7 +565,7 @@ dim3 persistent_grid_h3(Kernel kernel, const DeviceModel& m, int64_t units, int 
 
 hipError_t launch_blend_skin_h3(const DeviceModel& m, int64_t n, const float* features,
                                 const float* transforms, const float* trans, float* verts,
-                                float* vposed, hipStream_t stream) {
+                                hipStream_t stream) {
   // Sector-aligned rows as launch_blend_skin (mano_layout.h): verts phase
   // classes and the basis variant of each (MANO_H3_ALIGN 0: the plain layout).
   int lp = 0, aligned = 0;
@@ -558,13 +580,11 @@ hipError_t launch_blend_skin_h3(const DeviceModel& m, int64_t n, const float* fe
   const int64_t units = aligned_n_quads(n, lp, 7) * m.n_groups16;
   auto launch = [&](auto kernel) {
     hipLaunchKernelGGL(kernel, persistent_grid_h3(kernel, m, units, 1, kBlendSkinH3BlocksPerCU, 64 * kH3Waves),
-                       dim3(64 * kH3Waves), 0, stream, features, transforms, bh3, trans, verts, vposed,
+                       dim3(64 * kH3Waves), 0, stream, features, transforms, bh3, trans, verts,
                        n, m.n_verts, m.n_groups16, m.h3_vposed_unscale, m.h3_lbs_unscale, lp, shifts, aligned);
   };
-  if (trans && vposed) launch(blend_skin_h3_kernel<true, true>);
-  else if (trans) launch(blend_skin_h3_kernel<true, false>);
-  else if (vposed) launch(blend_skin_h3_kernel<false, true>);
-  else launch(blend_skin_h3_kernel<false, false>);
+  if (trans) launch(blend_skin_h3_kernel<true>);
+  else launch(blend_skin_h3_kernel<false>);
   return hipGetLastError();
 }
 

@@ -131,36 +131,47 @@ def test_large_batch_sampled(h3, dev, params):
 
 
 def test_matches_fp32_path(params, dev, h3):
-    """The two precision modes agree far inside the tolerance."""
+    """The two precision modes agree far inside the tolerance (verts-only
+    f16x3), and an f16x3 call that asks for rest_verts runs the exact-fp32
+    kernel: the same bits as the FP32 handle."""
     from mano_amd import ManoHip
     rng = np.random.default_rng(21)
     B = 2048
     betas = f32(rng.normal(0, 1, (B, 10)), dev)
     pose = f32(rng.normal(0, 0.6, (B, 16, 3)), dev)
     trans = f32(rng.uniform(-1, 1, (B, 3)), dev)
-    a = h3.forward(betas, pose, trans, rest_verts=True)
+    a = h3.forward(betas, pose, trans)
+    a_rv = h3.forward(betas, pose, trans, rest_verts=True)
     ref_engine = ManoHip(params, device=0)
     b = ref_engine.forward(betas, pose, trans, rest_verts=True)
     torch.cuda.synchronize()
     ref_engine.close()
     assert (a["verts"] - b["verts"]).abs().max().item() <= TOL_FP32CLASS
-    assert (a["rest_verts"] - b["rest_verts"]).abs().max().item() <= TOL_FP32CLASS
+    assert not torch.equal(a["verts"], b["verts"])      # the f16x3 kernel did run
+    assert torch.equal(a_rv["verts"], b["verts"]) and torch.equal(a_rv["rest_verts"], b["rest_verts"])
 
 
 @pytest.mark.parametrize("B", [1, 33, 200, 4096])
-def test_fused_lbs_equals_standalone(h3, dev, params, B):
-    """blend_skin_h3's LBS == skin_h3 on the v_posed it produced, bit for bit."""
+def test_fused_verts_vs_standalone_skin(h3, dev, params, B):
+    """blend_skin_h3 (verts only) and the f16x3 standalone LBS over the exact
+    fp32 v_posed (stage_blend) both stay within the fp32 class of the oracle;
+    they differ only by the GEMM's split products (no rest_verts output of the
+    f16x3 fused kernel exists to compare bit for bit: it is not built)."""
     rng = np.random.default_rng(100 + B)
     betas = f32(rng.normal(0, 1, (B, 10)), dev)
     pose = f32(rng.normal(0, 0.6, (B, 16, 3)), dev)
     trans = f32(rng.uniform(-1, 1, (B, 3)), dev)
-    fused = h3.forward(betas, pose, trans, rest_verts=True)
+    fused = h3.forward(betas, pose, trans)
+    vp = torch.empty((B, 778, 3), device=dev)
     v = torch.empty((B, 778, 3), device=dev)
     h3.stage_articulate(betas, pose, trans)
-    h3.stage_skin(B, v, rest_verts=fused["rest_verts"], trans=trans)
+    h3.stage_blend(B, rest_verts=vp)
+    h3.stage_skin(B, v, rest_verts=vp, trans=trans)
     torch.cuda.synchronize()
-    assert torch.equal(fused["verts"], v)
-    check({"verts": v}, mano_oracle.forward(params, host(betas), host(pose), host(trans)), f"B={B}")
+    ref = mano_oracle.forward(params, host(betas), host(pose), host(trans))
+    check({"verts": fused["verts"]}, ref, f"fused B={B}")
+    check({"verts": v}, ref, f"standalone B={B}")
+    assert (fused["verts"] - v).abs().max().item() <= TOL_FP32CLASS
 
 
 def test_standalone_skin_on_exact_vposed(h3, dev, params):
@@ -178,30 +189,23 @@ def test_standalone_skin_on_exact_vposed(h3, dev, params):
     check({"verts": v}, mano_oracle.forward(params, host(betas), host(pose)), "skin_h3")
 
 
-def test_rest_verts_launches_deterministic(h3, dev):
-    """The instantiation that once returned wrong hand-row-14/15 x coordinates
-    under load (blend_skin_h3 with rest_verts and trans): 40
-    back-to-back launches at 65,536 hands give the same bits as the first,
-    and the fused LBS equals the standalone one on that v_posed."""
+def test_verts_launches_deterministic(h3, dev):
+    """40 back-to-back f16x3 fused launches (with translation) at 65,536
+    hands give the same bits as the first: the kernel that remains once the
+    rest_verts instantiations are gone."""
     B = 65536
     inp = h3.synthetic_inputs(77, 0, B, trans=True)
     betas, pose, trans = inp["betas"], inp["pose"], inp["trans"]
     ref_v = torch.empty((B, 778, 3), device=dev)
-    ref_p = torch.empty_like(ref_v)
     h3.stage_articulate(betas, pose, trans)
-    h3.stage_blend_skin(B, ref_v, rest_verts=ref_p, trans=trans)
+    h3.stage_blend_skin(B, ref_v, trans=trans)
     v = torch.empty_like(ref_v)
-    p = torch.empty_like(ref_p)
     bad = 0
     for _ in range(40):
-        h3.stage_blend_skin(B, v, rest_verts=p, trans=trans)
-        bad += int(not torch.equal(v, ref_v)) + int(not torch.equal(p, ref_p))
+        h3.stage_blend_skin(B, v, trans=trans)
+        bad += int(not torch.equal(v, ref_v))
     torch.cuda.synchronize()
-    assert bad == 0, f"{bad} of 80 outputs differ from the first launch"
-    s = torch.empty_like(ref_v)
-    h3.stage_skin(B, s, rest_verts=ref_p, trans=trans)
-    torch.cuda.synchronize()
-    assert torch.equal(s, ref_v)
+    assert bad == 0, f"{bad} of 40 outputs differ from the first launch"
 
 
 @pytest.mark.parametrize("precision", ["fp32", "f16x3"])

@@ -507,7 +507,16 @@ def _phase_check(engine, dev, params, B):
     trans = f32(rng.uniform(-1, 1, (B, 3)), dev)
     n = B * 778 * 3
     for tr in (None, trans):
+        # plain-buffer references: with rest_verts (the fp32 kernel in either
+        # precision -- f16x3 has no rest_verts kernel), verts only (the
+        # precision's own fused kernel), and the standalone LBS over that v_posed
         want = engine.forward(betas, pose, tr, joints=False, rest_verts=True)
+        want_v = engine.forward(betas, pose, tr, joints=False)["verts"]
+        want_lbs = torch.empty_like(want_v)
+        engine.stage_skin(B, want_lbs, rest_verts=want["rest_verts"], trans=tr)
+        if engine.precision == "fp32":
+            torch.cuda.synchronize()
+            assert torch.equal(want_v, want["verts"]) and torch.equal(want_lbs, want["verts"])
         for off in range(8):
             buf = torch.full((2 * n + 64,), float("nan"), device=dev)
             v = buf[off:off + n].view(B, 778, 3)
@@ -529,14 +538,16 @@ def _phase_check(engine, dev, params, B):
             torch.cuda.synchronize()
             assert torch.equal(v, want["verts"]), (off, tr is None)
             assert torch.equal(vp, want["rest_verts"]), (off, tr is None)
-            assert torch.equal(v_only, want["verts"]), (off, tr is None)
+            assert torch.equal(v_only, want_v), (off, tr is None)
             if vp_blend is not None:
                 assert torch.equal(vp_blend, want["rest_verts"]), (off, tr is None, "blend")
-            assert torch.equal(v_lbs, want["verts"]), (off, tr is None, "unfused")
+            assert torch.equal(v_lbs, want_lbs), (off, tr is None, "unfused")
             assert torch.isnan(buf[:off]).all() and torch.isnan(buf[off + n:n + 32 + off]).all()
             assert torch.isnan(buf[2 * n + 32 + off:]).all()
     ref = mano_oracle.forward(params, host(betas), host(pose), host(trans))
     assert np.abs(host(want["verts"]) - ref["verts"]).max() <= TOL_M
+    assert np.abs(host(want_v) - ref["verts"]).max() <= TOL_M
+    assert np.abs(host(want_lbs) - ref["verts"]).max() <= TOL_M
 
 
 def truncated_params(params, V):
@@ -567,14 +578,17 @@ def test_other_mesh_sizes(dev, params, V, precision):
         pose = f32(rng.normal(0, 0.6, (B, 16, 3)), dev)
         trans = f32(rng.uniform(-1, 1, (B, 3)), dev)
         fused = m.forward(betas, pose, trans, joints=True, rest_verts=True)
+        fused_v = m.forward(betas, pose, trans)["verts"]   # the precision's verts-only kernel
         m.stage_articulate(betas, pose, trans)
         v = torch.empty((B, V, 3), device=dev)
         m.stage_skin(B, v, rest_verts=fused["rest_verts"], trans=trans)
         torch.cuda.synchronize()
-        assert torch.equal(fused["verts"], v)
+        if precision == "fp32":   # f16x3 builds no rest_verts kernel: its fused LBS has no v_posed to share
+            assert torch.equal(fused["verts"], v) and torch.equal(fused_v, v)
         ref = mano_oracle.forward(p, host(betas), host(pose), host(trans))
-        for key in ("verts", "joints", "rest_verts"):
-            err = np.abs(host(fused[key]) - ref[key]).max()
+        for key, got in (("verts", fused["verts"]), ("joints", fused["joints"]),
+                         ("rest_verts", fused["rest_verts"]), ("verts", fused_v), ("verts", v)):
+            err = np.abs(host(got) - ref[key]).max()
             assert err <= TOL_M, (V, precision, key, err)
     finally:
         m.close()
