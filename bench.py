@@ -155,6 +155,12 @@ def parse(argv=None):
                          "drop-in, CPU baseline) are shortened or skipped to end inside it")
     ap.add_argument("--inject-hang", type=int, default=None,
                     help="(tests, with --launch-check) this rank skips the collective and stalls")
+    ap.add_argument("--single-process", action="store_true",
+                    help="ONE process and host thread drive --gpus N devices (mano_amd.ManoMultiDevice; "
+                         "the gather is one RCCL group from that thread, ABI 6) instead of N torchrun ranks")
+    ap.add_argument("--devices", default=None,
+                    help="(--single-process) comma-separated device list (default 0..N-1; repeats allowed "
+                         "for a 1-GPU rehearsal, which assembles with peer copies instead of RCCL)")
     return ap.parse_args(argv)
 
 
@@ -587,6 +593,8 @@ def launch_check(args, wd):
 def main(argv=None):
     raw = sys.argv[1:] if argv is None else argv
     args = parse(raw)
+    if args.single_process:
+        return run_single_process(args)
     if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.force_pg):
         # Launch N ranks; this process never touches a GPU (it only waits).
         sys.exit(subprocess.run(launch_command(raw, args.gpus)).returncode)
@@ -615,6 +623,151 @@ def main(argv=None):
                                phases=wd.phases)
             print(json.dumps(line), file=sys.stdout if rank == 0 else sys.stderr, flush=True)
         raise
+
+
+def run_single_process(args):
+    """--single-process: one process and ONE host thread drive N devices
+    (mano_amd.multi_device.ManoMultiDevice).  A step = every device's forward
+    (articulate + blend_skin16 on its own stream, its contiguous shard of
+    hands r*B .. (r+1)*B - 1 of the counter-based batch) and, with the
+    workload's gather, the assembly of all verts + joints on device 0 by ONE
+    RCCL group issued from this thread (mano_group_start / mano_gather x N /
+    mano_group_end; peer copies when a device is listed twice).  Timed like
+    the process-per-GPU form: K steps between device-wide syncs of every GPU."""
+    import torch
+    from mano_amd import ManoMultiDevice, load_dump, synthetic_params
+    wl = WORKLOADS[args.workload]
+    B = args.batch if args.batch else wl["hands"]
+    n = args.gpus
+    devices = ([int(x) for x in args.devices.split(",")] if args.devices else list(range(n)))
+    if len(devices) != n:
+        raise SystemExit(f"--devices lists {len(devices)} devices for --gpus {n}")
+    gather = wl["gather"] if args.gather is None else args.gather
+    impl = "rccl" if len(set(devices)) == len(devices) else "copy"
+    with_trans = wl["trans"]
+    params = load_dump(args.model) if args.model else synthetic_params(0)
+    md = ManoMultiDevice(params, devices=devices, precision=args.precision)
+    n_total = B * n
+    ranges = md.shard_ranges(n_total)
+    inps = [e.synthetic_inputs(wl["seed"], a, b - a, trans=with_trans, stream=s)
+            for e, s, (a, b) in zip(md.engines, md.streams, ranges)]
+    outs, assembled = None, None
+    if gather:
+        _, outs, assembled = md._alloc_outputs(n_total, True, impl)
+    else:
+        outs = [{"verts": torch.empty((b - a, V, 3), device=torch.device("cuda", d)),
+                 "joints": torch.empty((b - a, 16, 3), device=torch.device("cuda", d))}
+                for d, (a, b) in zip(devices, ranges)]
+    for e, (a, b) in zip(md.engines, ranges):
+        e.workspace(b - a)
+    if gather and impl == "rccl":
+        md.comms()
+    keys = ["verts", "joints"]
+
+    def step(marks=None):
+        s0 = md.streams[0]
+        if marks is not None:
+            marks[0].record(s0)
+        for i, (e, s) in enumerate(zip(md.engines, md.streams)):
+            inp, o = inps[i], outs[i]
+            e.stage_articulate(inp["betas"], inp["pose"], inp.get("trans"), joints=o["joints"], stream=s)
+            if marks is not None and i == 0:
+                marks[1].record(s0)
+            e.stage_blend_skin(b_of(i), o["verts"], trans=inp.get("trans"), stream=s)
+            if marks is not None and i == 0:
+                marks[2].record(s0)
+        if gather:
+            if impl == "rccl":
+                md.comms().gather([[outs[i][k] for k in keys] for i in range(n)],
+                                  [assembled[k] for k in keys], 0, md.streams)
+            else:
+                for i in range(1, n):
+                    a, b = ranges[i]
+                    s0.wait_stream(md.streams[i])
+                    with torch.cuda.stream(s0):
+                        for k in keys:
+                            assembled[k][a:b].copy_(outs[i][k], non_blocking=True)
+                for i in range(1, n):
+                    md.streams[i].wait_stream(s0)   # the next step's writes follow the copies
+            if marks is not None:
+                marks[3].record(s0)
+
+    def b_of(i):
+        return ranges[i][1] - ranges[i][0]
+
+    def sync_all():
+        for d in sorted(set(devices)):
+            torch.cuda.synchronize(d)
+
+    t_ramp = time.perf_counter()
+    n_ramp = 0
+    while time.perf_counter() - t_ramp < args.ramp_seconds or n_ramp == 0:
+        for _ in range(10):
+            step()
+        n_ramp += 10
+        sync_all()
+    t_ramp = time.perf_counter() - t_ramp
+    for _ in range(args.warmup):
+        step()
+    sync_all()
+    every = max(1, min(args.event_every, args.steps // 5))
+    n_marks = 4 if gather else 3
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(n_marks)] if i % every == 0 else None
+              for i in range(args.steps)]
+    sync_all()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(events[i])
+    sync_all()
+    dt = time.perf_counter() - t0
+    sampled = [e for e in events if e is not None]
+    ms = {"articulate": float(np.mean([e[0].elapsed_time(e[1]) for e in sampled])),
+          "blend_skin": float(np.mean([e[1].elapsed_time(e[2]) for e in sampled]))}
+    if gather:
+        ms["gather"] = float(np.mean([e[2].elapsed_time(e[3]) for e in sampled]))
+    device_status = max(e.device_status(clear=True) for e in md.engines)
+    checks = []
+    if not args.no_check:
+        for i, e in enumerate(md.engines):
+            a, b = ranges[i]
+            src = ({k: assembled[k][a:b] for k in keys} if gather else outs[i])
+            checks.append(check_sample(e, wl["seed"], a, b - a, inps[i]["betas"], inps[i]["pose"],
+                                       inps[i].get("trans"), src["verts"], src["joints"], args.model,
+                                       with_trans))
+        correctness = merge_checks(checks)
+        correctness["pass"] = bool(correctness.get("pass")) and device_status == 0
+    else:
+        correctness = None
+    a_fl = FUSED_FLOP_PER_HAND * B / (ms["blend_skin"] * 1e-3) / 1e12 if args.precision == "fp32" else None
+    line = {
+        "metric": METRIC, "value": n_total * args.steps / dt, "unit": "hands/s", "n_gpus": n,
+        "steps": args.steps, "warmup": args.warmup, "ramp": {"seconds": t_ramp, "steps": n_ramp},
+        "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": args.precision,
+        "data": "synthetic (random-init MANO arrays of the official shapes, seed 0; Philox inputs keyed by "
+                "(seed, global hand index), generated on each device)",
+        "config": {"workload": wl["desc"] if B == wl["hands"] else f"{args.workload} at {B} hands per GPU",
+                   "hands_per_gpu": B, "global_batch": n_total, "outputs": "verts+joints", "trans": with_trans,
+                   "path": "forward", "gather_to_gpu0": bool(gather),
+                   "gather_impl": (None if not gather else
+                                   "one RCCL group of mano_gather from this thread" if impl == "rccl"
+                                   else "peer copies (a device listed twice)"),
+                   "parallelism": f"dp{n}"},
+        "process_model": {"single_process": True, "host_threads": 1, "devices": devices,
+                          "streams": "one per device", "comm": "mano_comm_create_all" if gather and impl == "rccl"
+                          else None},
+        "kernels_device0": {k: {"ms": v} for k, v in ms.items()},
+        "roofline": ({"kernel": "blend_skin16_kernel", "bound": "mfma", "achieved": a_fl,
+                      "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": a_fl / PEAK_FP32_TFLOPS,
+                      "algorithmic_per_hand": FUSED_FLOP_PER_HAND, "device": devices[0]} if a_fl else None),
+        "correctness": correctness, "device_status": device_status, "status": "ok",
+        "run": {"wall_s": round(time.monotonic() - T_START, 3)},
+    }
+    if gather and n > 1:
+        line["gather"] = gather_stats("sendrecv", n, B, ms["gather"])
+        line["gather"]["form"] = line["config"]["gather_impl"]
+    print(json.dumps(line), flush=True)
+    md.close()
 
 
 def run(args, wd):

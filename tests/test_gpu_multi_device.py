@@ -141,3 +141,29 @@ def test_two_devices_rccl_group_gather(params):
         assert torch.equal(out["verts"].cpu(), ref["verts"]) and torch.equal(out["joints"].cpu(), ref["joints"])
     finally:
         md.close()
+
+
+@pytest.mark.parametrize("extra", [["--gpus", "1", "--workload", "C4", "--batch", "8192"],
+                                   ["--gpus", "3", "--devices", "0,0,0", "--workload", "C4", "--batch", "4096"],
+                                   ["--gpus", "2", "--devices", "0,0", "--batch", "4096"]])
+def test_bench_single_process(extra):
+    """bench.py --single-process: one host thread drives the devices (one RCCL
+    group gather at n = 1; peer-copy assembly with one GPU listed several
+    times), every device's sampled hands pass the oracle check."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from conftest import REPO
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--single-process", *extra,
+                        "--steps", "10", "--warmup", "2", "--ramp-seconds", "0.2"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    n = int(extra[1])
+    assert line["status"] == "ok" and line["n_gpus"] == n and line["value"] > 0
+    assert line["process_model"]["single_process"] and line["process_model"]["host_threads"] == 1
+    assert line["correctness"]["pass"] and line["correctness"]["ranks_checked"] == n, line["correctness"]
+    if "C4" in extra:
+        assert line["config"]["gather_to_gpu0"]
+        assert ("RCCL" in line["config"]["gather_impl"]) == (n == 1)
