@@ -18,7 +18,7 @@
     defined(MANO_BLEND_STORE_POLICY) || defined(MANO_BLEND_COUNTED) ||           \
     defined(MANO_BS_STORE_PRIO) || defined(MANO_H3_ABLATE) || defined(MANO_H3_ALIGN) || defined(MANO_H3_ASM_MFMA) ||         \
     defined(MANO_H3_BLOCKS) || defined(MANO_H3_DMA_PRIO) || defined(MANO_H3_FULL_WAIT) ||          \
-    defined(MANO_H3_NO_PACK) || defined(MANO_H3_NT_STORE) || defined(MANO_H3_RING) || defined(MANO_H3_SCALAR_UNSCALE) ||    \
+    defined(MANO_H3_NO_PACK) || defined(MANO_H3_NT_STORE) || defined(MANO_H3_RING) || defined(MANO_H3_SPLIT_ACC) || defined(MANO_H3_SCALAR_UNSCALE) ||    \
     defined(MANO_H3_SKIN_PAIR) || defined(MANO_H3_TPW) || defined(MANO_H3_WAVES) ||                \
     defined(MANO_PAIR_POLL_LIMIT) || defined(MANO_PAIR_ALIGN) || defined(MANO_PAIR_NT) || defined(MANO_PAIR_REVERSE) || defined(MANO_PAIR_SLEEP_CMP) || defined(MANO_PAIR_SLEEP_MEM) || \
     defined(MANO_PAIR_SLOTS) || defined(MANO_PAIR_STAMP) || defined(MANO_QUAD_ABLATE) ||           \

@@ -271,6 +271,9 @@ constexpr int kH3BlocksPerCU = MANO_H3_BLOCKS;
 #ifndef MANO_H3_RING
 #define MANO_H3_RING 2
 #endif
+#ifndef MANO_H3_SPLIT_ACC
+#define MANO_H3_SPLIT_ACC 0  // blend_skin_h3: one LDS read per B fragment, two accumulators
+#endif
 // LDS slots of blend_skin_h3's basis ring (32 KB each; groups staged ahead =
 // kH3Ring - 1).  160 KB of LDS per CU holds at most 4 with one block per CU.
 constexpr int kH3Ring = MANO_H3_RING;
@@ -388,9 +391,45 @@ __global__ __launch_bounds__(64 * kH3Waves, kH3BlocksPerCU) void blend_skin_h3_k
         if constexpr (MANO_H3_DMA_PRIO != 0) __builtin_amdgcn_s_setprio(0);
       }
       const f16x8* L = ring + slot * kSlot + lane;
+      f32x4 p[kH3TPW][3];
+#if MANO_H3_SPLIT_ACC
+      // Each K-step's two B fragments of a coordinate (lo and hi halves) are
+      // read from LDS once and feed all three products: the small ones (hi.lo,
+      // lo.hi) into one accumulator, hi.hi into a second, added at the end --
+      // 30 fragment reads per group instead of 45.
+      {
+        f32x4 pb[kH3TPW][3];
+#pragma unroll
+        for (int s = 0; s < kH3Steps; ++s)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const f16x8 b_lo = L[((2 * c + 1) * kH3Steps + s) * 64];
+            const f16x8 b_hi = L[((2 * c) * kH3Steps + s) * 64];
+#pragma unroll
+            for (int t = 0; t < kH3TPW; ++t) {
+              if (s == 0) {
+                mfma_init(p[t][c], xh[t][0], b_lo);
+                mfma_init(pb[t][c], xh[t][0], b_hi);
+              } else {
+                mfma_acc(p[t][c], xh[t][s], b_lo);
+                mfma_acc(pb[t][c], xh[t][s], b_hi);
+              }
+              mfma_acc(p[t][c], xl[t][s], b_hi);
+            }
+          }
+#pragma unroll
+        for (int t = 0; t < kH3TPW; ++t) {
+          mfma_fence(p[t]);
+          mfma_fence(pb[t]);
+#pragma unroll
+          for (int c = 0; c < 3; ++c)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) p[t][c][r] = no_pack(p[t][c][r] + pb[t][c][r]);
+        }
+      }
+#else
       // The coordinates' (and tiles') chains interleaved (independent
       // accumulators), each summing hi.lo, lo.hi, then hi.hi over the 5 K-steps.
-      f32x4 p[kH3TPW][3];
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
         const f16x8 b = L[((2 * c + 1) * kH3Steps) * 64];
@@ -421,6 +460,7 @@ __global__ __launch_bounds__(64 * kH3Waves, kH3BlocksPerCU) void blend_skin_h3_k
 #pragma unroll
           for (int t = 0; t < kH3TPW; ++t) mfma_acc(p[t][c], xh[t][s], b);
         }
+#endif
       // the lane's vertex in this group (grp, shift uniform: scalar branches)
       int vx;
       if (aligned) {
