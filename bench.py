@@ -154,7 +154,8 @@ def parse(argv=None):
                     help="wall-time budget from process start: rank 0's host legs (PMC passes, "
                          "drop-in, CPU baseline) are shortened or skipped to end inside it")
     ap.add_argument("--inject-hang", type=int, default=None,
-                    help="(tests, with --launch-check) this rank skips the collective and stalls")
+                    help="(tests) this rank skips a collective and stalls: the launch check's all_reduce, "
+                         "or with a process group the clock ramp's")
     ap.add_argument("--single-process", action="store_true",
                     help="ONE process and host thread drive --gpus N devices (mano_amd.ManoMultiDevice; "
                          "the gather is one RCCL group from that thread, ABI 6) instead of N torchrun ranks")
@@ -911,6 +912,9 @@ def run(args, wd):
         n_ramp += 10
         torch.cuda.synchronize()
         done = time.perf_counter() - t_ramp >= args.ramp_seconds
+        if args.inject_hang == rank and dist_on:
+            while True:       # (tests) this rank stalls outside the ramp's collective
+                time.sleep(0.5)
         if dist_on:
             flag = torch.tensor([1 if done else 0], device=dev if args.backend == "nccl" else "cpu",
                                 dtype=torch.int32)

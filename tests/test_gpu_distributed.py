@@ -279,3 +279,48 @@ def test_bench_c4_ramp_ends_together():
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert line["ramp"]["steps"] > 10, line["ramp"]
     assert line["gather_check"]["bit_exact"]
+
+
+def test_bench_watchdog_in_a_gpu_run():
+    """The watchdog inside a real GPU run: 2 gloo ranks sharing the GPU, rank 1
+    stalls outside the clock ramp's all_reduce (--inject-hang 1): rank 0
+    prints the status line naming the phase ("ramp") with its phase history,
+    both ranks' Python stacks reach stderr, the launcher exits non-zero, all
+    well inside the watchdog budget given."""
+    import json
+    import subprocess
+    import time
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                        "--batch", "1024", "--steps", "5", "--warmup", "1", "--ramp-seconds", "0.2",
+                        "--no-cpu", "--no-extra", "--no-dropin", "--no-live-pmc",
+                        "--inject-hang", "1", "--watchdog-seconds", "45", "--pg-timeout-seconds", "200"],
+                       capture_output=True, text=True, timeout=170, env=env)
+    wall = time.monotonic() - t0
+    assert r.returncode != 0
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["status"] == "watchdog" and line["phase"] == "ramp" and line["value"] is None
+    assert [p[0] for p in line["phases"]][:3] == ["init_process_group", "model_create", "ramp"]
+    assert "rank 0/2: watchdog" in r.stderr and r.stderr.count("in run") >= 2
+    assert wall < 150
+
+
+def test_bench_deadline_skips_rank0_legs():
+    """--deadline-seconds too short for rank 0's host legs: the line still
+    lands (status ok) with every leg it could not fit listed in
+    run.skipped_legs, and the timed numbers intact."""
+    import json
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--batch", "4096", "--steps", "10",
+                        "--warmup", "2", "--ramp-seconds", "0.2", "--no-extra", "--deadline-seconds", "35"],
+                       capture_output=True, text=True, timeout=200)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["status"] == "ok" and line["value"] > 0 and line["correctness"]["pass"]
+    sk = line["run"]["skipped_legs"]
+    assert set(sk) == {"live_pmc", "dropin", "cpu_baseline"}, sk
+    assert "cpu_baseline" not in line and "dropin" not in line
+    assert line["roofline"]["traffic"] is not None            # the committed PMC summary stands in
+    assert "skipped" in line["roofline"]["traffic_source"]
+    assert line["run"]["wall_s"] < 60
