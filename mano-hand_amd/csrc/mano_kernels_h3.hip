@@ -399,12 +399,30 @@ __global__ __launch_bounds__(64 * kH3Waves, kH3BlocksPerCU) void blend_skin_h3_k
       // 30 fragment reads per group instead of 45.
       {
         f32x4 pb[kH3TPW][3];
+        // MANO_H3_SPLIT_ACC 2: step s + 1's six fragments are read before
+        // step s's MFMAs (pinned by scheduling barriers), so an MFMA waits on
+        // a read issued a whole step earlier, not on the one just before it.
+        f16x8 cur_lo[3], cur_hi[3];
 #pragma unroll
-        for (int s = 0; s < kH3Steps; ++s)
+        for (int c = 0; c < 3; ++c) {
+          cur_lo[c] = L[((2 * c + 1) * kH3Steps) * 64];
+          cur_hi[c] = L[((2 * c) * kH3Steps) * 64];
+        }
+#pragma unroll
+        for (int s = 0; s < kH3Steps; ++s) {
+          f16x8 nxt_lo[3], nxt_hi[3];
+          if (MANO_H3_SPLIT_ACC >= 2 && s + 1 < kH3Steps) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              nxt_lo[c] = L[((2 * c + 1) * kH3Steps + s + 1) * 64];
+              nxt_hi[c] = L[((2 * c) * kH3Steps + s + 1) * 64];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
 #pragma unroll
           for (int c = 0; c < 3; ++c) {
-            const f16x8 b_lo = L[((2 * c + 1) * kH3Steps + s) * 64];
-            const f16x8 b_hi = L[((2 * c) * kH3Steps + s) * 64];
+            const f16x8 b_lo = MANO_H3_SPLIT_ACC >= 2 ? cur_lo[c] : L[((2 * c + 1) * kH3Steps + s) * 64];
+            const f16x8 b_hi = MANO_H3_SPLIT_ACC >= 2 ? cur_hi[c] : L[((2 * c) * kH3Steps + s) * 64];
 #pragma unroll
             for (int t = 0; t < kH3TPW; ++t) {
               if (s == 0) {
@@ -417,6 +435,15 @@ __global__ __launch_bounds__(64 * kH3Waves, kH3BlocksPerCU) void blend_skin_h3_k
               mfma_acc(p[t][c], xl[t][s], b_hi);
             }
           }
+          if (MANO_H3_SPLIT_ACC >= 2 && s + 1 < kH3Steps) {
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              cur_lo[c] = nxt_lo[c];
+              cur_hi[c] = nxt_hi[c];
+            }
+          }
+        }
 #pragma unroll
         for (int t = 0; t < kH3TPW; ++t) {
           mfma_fence(p[t]);
