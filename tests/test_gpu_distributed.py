@@ -295,7 +295,7 @@ def test_bench_watchdog_in_a_gpu_run():
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo",
                         "--batch", "1024", "--steps", "5", "--warmup", "1", "--ramp-seconds", "0.2",
                         "--no-cpu", "--no-extra", "--no-dropin", "--no-live-pmc",
-                        "--inject-hang", "1", "--watchdog-seconds", "45", "--pg-timeout-seconds", "200"],
+                        "--inject-hang", "1", "--watchdog-seconds", "30", "--pg-timeout-seconds", "200"],
                        capture_output=True, text=True, timeout=170, env=env)
     wall = time.monotonic() - t0
     assert r.returncode != 0
