@@ -197,6 +197,38 @@ class ManoMultiDevice:
                 eng.forward(bt, take(pose), take(trans), joints=joints, out=per[i], stream=s)
         return self._finish(ranges, per, assembled, joints, gather)
 
+    def forward_pca(self, betas: torch.Tensor, pca: torch.Tensor, rot: Optional[torch.Tensor] = None,
+                    trans: Optional[torch.Tensor] = None, *, joints: bool = True, gather="rccl"):
+        """Batched set_params(pose_pca=c, global_rot=rot, shape=beta)
+        (mano_np.py:66-77) split over the devices: ManoHip.forward_pca per
+        shard.  pca (B,N) or (N,) shared, rot (B,3) / (3,) shared / None,
+        betas (B,10) / (10,); outputs as in `forward`."""
+        if gather not in ("rccl", "copy", False, None):
+            raise ValueError(f"gather must be 'rccl', 'copy' or False, got {gather!r}")
+        gather = gather or False
+        B = pca.shape[0] if pca.dim() == 2 else (betas.shape[0] if betas.dim() == 2 else None)
+        if B is None:
+            raise ValueError("batch size unknown: give (B,N) pca or (B,10) betas")
+        ranges, per, assembled = self._alloc_outputs(B, joints, gather)
+        src = next((t for t in (pca, betas, rot, trans) if t is not None and t.is_cuda), None)
+        src_stream = torch.cuda.current_stream(src.device) if src is not None else None
+        for i, (eng, d, s) in enumerate(zip(self.engines, self.devices, self.streams)):
+            a, b = ranges[i]
+            if b == a:
+                continue
+            dev = torch.device("cuda", d)
+            if src_stream is not None:
+                s.wait_stream(src_stream)
+            with torch.cuda.device(dev), torch.cuda.stream(s):
+                def take(t, per_hand):
+                    if t is None:
+                        return None
+                    return (t[a:b] if per_hand else t).to(dev, non_blocking=True).contiguous()
+                eng.forward_pca(take(betas, betas.dim() == 2), take(pca, pca.dim() == 2),
+                                take(rot, rot is not None and rot.dim() == 2 and rot.shape[0] == B),
+                                take(trans, True), joints=joints, out=per[i], stream=s)
+        return self._finish(ranges, per, assembled, joints, gather)
+
     def forward_synthetic(self, seed: int, n_total: int, *, trans: bool = False, joints: bool = True,
                           gather="rccl"):
         """The forward of global hands 0..n_total-1 of the counter-based

@@ -127,6 +127,40 @@ def test_host_inputs_and_shared_betas(params):
         m.close()
 
 
+@pytest.mark.parametrize("devices,gather,n_pca,rot_kind", [([0], "rccl", 45, "per_hand"),
+                                                           ([0, 0, 0], "copy", 6, "shared"),
+                                                           ([0, 0], False, 12, None)])
+def test_forward_pca_split(params, devices, gather, n_pca, rot_kind):
+    """forward_pca (mano_np.py:66-77 batched) split over the devices equals
+    the single-handle forward_pca bit for bit: per-hand / shared / absent
+    global rotation, 45 / 6 / 12 coefficients, per-hand betas and trans."""
+    from mano_amd import ManoHip, ManoMultiDevice
+    from mano_amd.distributed import shard_range
+    rng = np.random.default_rng(n_pca)
+    n = 1001
+    d = torch.device("cuda", 0)
+    t = lambda a: torch.tensor(a, dtype=torch.float32, device=d)  # noqa: E731
+    betas, pca = t(rng.normal(0, 1, (n, 10))), t(rng.normal(0, 1, (n, n_pca)))
+    trans = t(rng.normal(0, 0.1, (n, 3)))
+    rot = {"per_hand": t(rng.normal(0, 0.7, (n, 3))), "shared": t(rng.normal(0, 0.7, 3)), None: None}[rot_kind]
+    m = ManoHip(params, device=0)
+    ref = m.forward_pca(betas, pca, rot, trans, joints=True)
+    torch.cuda.synchronize()
+    md = ManoMultiDevice(params, devices=devices)
+    try:
+        out = md.forward_pca(betas, pca, rot, trans, gather=gather)
+        md.synchronize()
+        if gather:
+            assert torch.equal(out["verts"], ref["verts"]) and torch.equal(out["joints"], ref["joints"])
+        else:
+            for i, o in enumerate(out):
+                a, b = shard_range(n, i, len(devices))
+                assert torch.equal(o["verts"], ref["verts"][a:b]) and torch.equal(o["joints"], ref["joints"][a:b])
+    finally:
+        md.close()
+        m.close()
+
+
 @pytest.mark.skipif(torch.cuda.device_count() < 2, reason="the RCCL group gather needs 2 GPUs")
 def test_two_devices_rccl_group_gather(params):
     """n = 2 for real: one thread, two GPUs, one RCCL group; GPU 0's
