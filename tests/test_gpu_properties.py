@@ -14,7 +14,6 @@ kernel's layout (mano_layout.h) cannot hide between the samples:
   joint's transform from the left, so verts(root r) = R(r)(verts(root 0) -
   J_0) + J_0 and the same for the posed joints (float64 on the fp32 outputs,
   within the north_star 1e-5 m)."""
-import numpy as np
 import pytest
 
 from oracle import mano_oracle
