@@ -13,7 +13,7 @@
 #pragma once
 
 #if !defined(MANO_DIAGNOSTIC_BUILD)
-#if  defined(MANO_BS_ABLATE) || defined(MANO_BS_ALIGN) || defined(MANO_BS_BLOCKS_PER_CU) ||   \
+#if  defined(MANO_BS_ABLATE) || defined(MANO_BS_ACC2) || defined(MANO_BS_ALIGN) || defined(MANO_BS_BLOCKS_PER_CU) ||   \
     defined(MANO_BS_DMA_PRIO) || defined(MANO_BS_NT_STORE) || defined(MANO_BS_REST_NT) || defined(MANO_BS_STAMP) || \
     defined(MANO_BLEND_STORE_POLICY) || defined(MANO_BLEND_COUNTED) ||           \
     defined(MANO_BS_STORE_PRIO) || defined(MANO_H3_ABLATE) || defined(MANO_H3_ALIGN) || defined(MANO_H3_ASM_MFMA) ||         \

@@ -197,9 +197,49 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 // LDS read of K-group g + 1 issued before group g's four MFMAs and pinned
 // there by a scheduling barrier.  hook() is issued after K-group kAt (pinned
 // between the groups' MFMAs the same way; kAt < 0: none).
+// MANO_BS_ACC2=1 (diagnostic builds): two accumulators, K-steps 0..19 and
+// 20..36, issued alternately so a wave alone in its MFMA phase is not held to
+// one MFMA per 40-cycle dependent latency (the 16x16x4 issue interval is 32),
+// summed at the end (changes the rounding order: not bit-identical to the
+// unfused blend GEMM).
+#ifndef MANO_BS_ACC2
+#define MANO_BS_ACC2 0
+#endif
 template <int kAt, typename Hook>
 __device__ __forceinline__ f32x4 mfma16_tile_hook(const float (&a)[kGroups16 * 4],
                                                   const f32x4* __restrict__ b, int lane, Hook&& hook) {
+#if MANO_BS_ACC2
+  constexpr int kHalf = (kGroups16 + 1) / 2;  // K-groups of the first accumulator
+  f32x4 acc0 = {}, acc1 = {};
+  f32x4 bn0 = b[lane], bn1 = b[kHalf * 64 + lane];
+#pragma unroll
+  for (int g = 0; g < kHalf; ++g) {
+    const int g1 = kHalf + g;
+    const f32x4 bv0 = bn0, bv1 = bn1;
+    if (g + 1 < kHalf) bn0 = b[(g + 1) * 64 + lane];
+    if (g1 + 1 < kGroups16) bn1 = b[(g1 + 1) * 64 + lane];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[4 * g + q], bv0[q], acc0, 0, 0, 0);
+      if (g1 < kGroups16 && 4 * g1 + q < kSteps16)
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[4 * g1 + q], bv1[q], acc1, 0, 0, 0);
+    }
+    if (g == kAt) {
+      __builtin_amdgcn_sched_barrier(0);
+      hook();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  f32x4 sum;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float s = acc0[r] + acc1[r];
+    asm volatile("" : "+v"(s));  // scalar adds (no v_pk_add_f32 beside the MFMAs)
+    sum[r] = s;
+  }
+  return sum;
+#else
   f32x4 acc = {};
   f32x4 bn = b[lane];
 #pragma unroll
@@ -217,6 +257,7 @@ __device__ __forceinline__ f32x4 mfma16_tile_hook(const float (&a)[kGroups16 * 4
     }
   }
   return acc;
+#endif
 }
 __device__ __forceinline__ f32x4 mfma16_tile(const float (&a)[kGroups16 * 4], const f32x4* __restrict__ b,
                                              int lane) {
