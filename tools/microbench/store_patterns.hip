@@ -95,6 +95,41 @@ __global__ __launch_bounds__(256) void win32(float* __restrict__ out, long n) {
   }
 }
 
+// rows12set: blend_skin_h3's order -- a block of 8 waves holds 8 16-hand
+// tiles (128 consecutive hands) and walks the 49 groups; at a time its waves
+// write the same 192-B column span of 128 rows.
+__global__ __launch_bounds__(512) void rows12set(float* __restrict__ out, long n) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4, col = lane & 15;
+  long u, ue;
+  range((n / 128) * NG, blockIdx.x, gridDim.x, u, ue);
+  for (; u < ue; ++u) {
+    const long set = u / NG; const int g = int(u - set * NG);
+    const int vb = min(16 * g, NV - 16);
+    float* base = out + (set * 128 + wave * 16) * VS + 3 * (vb + col);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      *reinterpret_cast<f32x3*>(base + (4 * q + r) * VS) = f32x3{float(u), float(r), float(lane)};
+  }
+}
+
+// rows12vs: the vertex-stationary order -- a block of 7 waves owns 7
+// consecutive groups (set b % 7 of the 49) and walks a range of 16-hand
+// tiles; at a time its waves write one 1,344-B span of each of 16 rows.
+__global__ __launch_bounds__(448) void rows12vs(float* __restrict__ out, long n) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4, col = lane & 15;
+  const int gset = blockIdx.x % 7;
+  const long nr = gridDim.x / 7;
+  long t, te;
+  range(n / 16, blockIdx.x / 7, nr, t, te);
+  const int vb = min(16 * (7 * gset + wave), NV - 16);
+  for (; t < te; ++t) {
+    float* base = out + t * 16 * VS + 3 * (vb + col);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      *reinterpret_cast<f32x3*>(base + (4 * q + r) * VS) = f32x3{float(t), float(r), float(lane)};
+  }
+}
+
 __global__ __launch_bounds__(256) void flat16(f32x4* __restrict__ out, long n4) {
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += gridDim.x * 256L) out[i] = f32x4{1, 2, 3, float(i)};
 }
@@ -153,6 +188,14 @@ int main() {
     timeit(nm, W, [&] { hipLaunchKernelGGL(win32, dim3(g), dim3(256), 0, 0, b, n); });
     snprintf(nm, 64, "copy12 (%d blk/CU)", bpc);
     timeit(nm, 2 * W, [&] { hipLaunchKernelGGL(copy12, dim3(g), dim3(256), 0, 0, a, b, n); });
+  }
+  for (int bpc : {1, 2}) {
+    char nm[64];
+    snprintf(nm, 64, "rows12set (%d blk/CU, 8 waves)", bpc);
+    timeit(nm, W, [&] { hipLaunchKernelGGL(rows12set, dim3(ncu * bpc), dim3(512), 0, 0, b, n); });
+    const unsigned gvs = unsigned((ncu * bpc) / 7 * 7);
+    snprintf(nm, 64, "rows12vs (%u blk, 7 waves)", gvs);
+    timeit(nm, W, [&] { hipLaunchKernelGGL(rows12vs, dim3(gvs), dim3(448), 0, 0, b, n); });
   }
   timeit("flat16", W, [&] { hipLaunchKernelGGL(flat16, dim3(ncu * 8), dim3(256), 0, 0, (f32x4*)b, long(nf / 4)); });
   timeit("copy16", 2 * W, [&] { hipLaunchKernelGGL(copy16, dim3(ncu * 8), dim3(256), 0, 0, (const f32x4*)a, (f32x4*)b, long(nf / 4)); });
