@@ -94,6 +94,45 @@ WORKLOADS = {
 }
 
 
+# The BASELINE configs that need a multi-GPU node (configs[2] and [3]), run at
+# every N > 1 as legs after the C2 headline: the GLOBAL batch is fixed and
+# split over the ranks (strong scaling), keyed by global hand index.
+LEGS = {
+    "C3": {"global": 2 ** 24, "seed": 1002, "gather": False,
+           "desc": "C3: 16,777,216 hands (2^24) data-parallel over the ranks, per-shard verts + joints "
+                   "(no collective)"},
+    "C4": {"global": 2 ** 22, "seed": 1003, "gather": True,
+           "desc": "C4: 4,194,304 hands (2^22) over the ranks + gather of every rank's verts + joints to GPU 0"},
+}
+
+
+def parse_leg_global(text):
+    """'C3=8192,C4=4096' -> {"C3": 8192, "C4": 4096} (--leg-global)."""
+    out = {}
+    for item in filter(None, (x.strip() for x in (text or "").split(","))):
+        name, _, val = item.partition("=")
+        if name not in LEGS or not val.isdigit() or int(val) < 1:
+            raise SystemExit(f"--leg-global: bad item {item!r} (want C3=N or C4=N, N >= 1)")
+        out[name] = int(val)
+    return out
+
+
+def plan_legs(args, world):
+    """The legs this run takes and each rank's shard of them (empty at one
+    rank unless --legs on)."""
+    if args.legs == "off" or (args.legs == "auto" and world <= 1):
+        return {}
+    from mano_amd.distributed import shard_range
+    over = parse_leg_global(args.leg_global)
+    plan = {}
+    for name, spec in LEGS.items():
+        n = over.get(name, spec["global"])
+        plan[name] = {"desc": spec["desc"], "global_batch": n, "baseline_size": n == spec["global"],
+                      "seed": spec["seed"], "gather_to_gpu0": spec["gather"], "scaling": "strong",
+                      "hands_per_rank": [b - a for a, b in (shard_range(n, r, world) for r in range(world))]}
+    return plan
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -159,6 +198,19 @@ def parse(argv=None):
     ap.add_argument("--single-process", action="store_true",
                     help="ONE process and host thread drive --gpus N devices (mano_amd.ManoMultiDevice; "
                          "the gather is one RCCL group from that thread, ABI 6) instead of N torchrun ranks")
+    ap.add_argument("--legs", choices=("auto", "on", "off"), default="auto",
+                    help="the multi-GPU configs as untimed legs after the headline (BASELINE configs[2..3]: "
+                         "C3 = 2^24 hands strong-scaled over the ranks, C4 = 2^22 hands + the gather to GPU 0); "
+                         "auto = on when WORLD_SIZE > 1.  Not part of `value`")
+    ap.add_argument("--leg-global", default="",
+                    help="(tests) override a leg's global batch, e.g. C3=8192,C4=4096 (the line then says "
+                         "baseline_size false)")
+    ap.add_argument("--leg-steps", type=int, default=5,
+                    help="timed steps per leg (after one untimed step); the gloo form of C4 runs its "
+                         "host-memory gather once")
+    ap.add_argument("--leg-min-seconds", type=float, default=90.0,
+                    help="a leg starts only with this many seconds left before --watchdog-seconds "
+                         "(rank-agreed); otherwise it is named in run.skipped_legs")
     ap.add_argument("--devices", default=None,
                     help="(--single-process) comma-separated device list (default 0..N-1; repeats allowed "
                          "for a 1-GPU rehearsal, which assembles with peer copies instead of RCCL)")
@@ -438,22 +490,28 @@ def merge_checks(per_rank):
     return out
 
 
-def check_gather(model, seed, B, world, gv, gj, with_trans, per_rank=64):
+def check_gather(model, seed, B, world, gv, gj, with_trans, per_rank=64, ranges=None):
     """GPU 0's gathered buffers vs a local forward: from every rank's range
-    [r B, (r + 1) B) the first 16, last 16 and a random run of 32 hands are
-    regenerated by global index and forwarded on this GPU; the rows must equal
-    gv / gj bit for bit (hands are independent, mano_np.py:79-115)."""
+    [r B, (r + 1) B) (or `ranges[r]`) the first 16, last 16 and a random run
+    of 32 hands are regenerated by global index and forwarded on this GPU; the
+    rows must equal gv / gj bit for bit (hands are independent,
+    mano_np.py:79-115)."""
     import torch
     rng = np.random.default_rng(1)
     bad, n, ranks_bad = 0, 0, []
-    for r in range(world):
+    if ranges is None:
+        ranges = [(r * B, (r + 1) * B) for r in range(world)]
+    for r, (first, stop) in enumerate(ranges):
+        B = stop - first
+        if B <= 0:
+            continue
         k = min(16, B)
         runs = [(0, k), (max(0, B - k), k)]
         if B > 32:
             runs.append((int(rng.integers(0, B - 32)), 32))
         wrong = 0
         for off, cnt in runs:
-            g0 = r * B + off
+            g0 = first + off
             inp = model.synthetic_inputs(seed, g0, cnt, trans=with_trans)
             out = model.forward(inp["betas"], inp["pose"], inp.get("trans"), joints=True)
             dv = (out["verts"] != gv[g0:g0 + cnt]).flatten(1).any(1)
@@ -468,6 +526,190 @@ def check_gather(model, seed, B, world, gv, gj, with_trans, per_rank=64):
             "bit_exact": bad == 0,
             "method": "rank 0 regenerates each rank's first 16, last 16 and 32 random consecutive hands "
                       "by global index, forwards them locally, compares with GPU 0's gathered verts / joints"}
+
+
+def run_legs(args, plan, model, rank, world, dev, local_dev, wd, skipped):
+    """BASELINE's multi-GPU configs, after the headline (not part of `value`).
+
+    C3: the 2^24-hand global batch split over the ranks (rank r: hands
+    shard_range(2^24, r, N), Philox seed 1002 by global index), the forward
+    (mano_forward: articulate + blend_skin16) timed over --leg-steps between a
+    barrier + device sync on both sides, max over ranks -> whole-node hands/s
+    at fixed total work; every rank's sampled hands vs the float64 oracle.
+    C4: the 2^22-hand batch the same way, each step = forward + the gather of
+    every rank's verts + joints to GPU 0 (nccl: mano_gather, one RCCL group of
+    peer -> GPU 0 sends over xGMI, GPU 0's shard computed in place; the ring
+    mano_allgather timed after it as the comparison; gloo rehearsal: the same
+    layout through host memory in bounded pieces, once); GPU 0's rows of every
+    rank's range checked bit for bit against hands regenerated by global index.
+    Every rank runs this (collectives); returns rank 0's report."""
+    import torch
+    import torch.distributed as dist
+    from mano_amd.distributed import AbiGather, gather_rows_to_root, shard_range
+    nccl = args.backend == "nccl"
+    red_dev = dev if nccl else "cpu"
+    out, gatherer = {}, None
+    last_note = [0.0]
+
+    def note(done, total):
+        # a progress line on stderr at most every 20 s (rank 0): a long host
+        # gather is not mistaken for a hang
+        if rank == 0 and time.monotonic() - last_note[0] > 20.0:
+            last_note[0] = time.monotonic()
+            print(f"bench: {wd.phase}: gathered {done} of {total} rows per rank "
+                  f"({time.monotonic() - T_START:.0f} s)", file=sys.stderr, flush=True)
+    for name, p in plan.items():
+        # the ranks agree to start a leg (it must end before the watchdog)
+        left = (T_START + args.watchdog_seconds - time.monotonic()) if args.watchdog_seconds > 0 else 1e9
+        go = torch.tensor([1 if left >= args.leg_min_seconds else 0], device=red_dev, dtype=torch.int32)
+        dist.all_reduce(go, op=dist.ReduceOp.MIN)
+        if not int(go.item()):
+            skipped[f"leg_{name}"] = (f"{left:.0f} s left before --watchdog-seconds on rank {rank} "
+                                      f"(a leg needs --leg-min-seconds {args.leg_min_seconds:.0f})")
+            continue
+        wd.enter(f"leg_{name}")
+        if rank == 0:
+            print(f"bench: leg {name}: {p['global_batch']} hands over {world} ranks "
+                  f"({time.monotonic() - T_START:.0f} s)", file=sys.stderr, flush=True)
+        t_leg = time.monotonic()
+        n_total, seed, gather = p["global_batch"], p["seed"], p["gather_to_gpu0"]
+        a, b = shard_range(n_total, rank, world)
+        Bl = b - a
+        inp = model.synthetic_inputs(seed, a, Bl)
+        # the forward's own workspace (1,408 B per hand), freed after the leg
+        ws = torch.empty(model.forward_workspace_bytes(max(Bl, 1)) + 256, dtype=torch.uint8, device=dev)
+        gv = gj = None
+        if gather and rank == 0:
+            gv = torch.empty((n_total, V, 3), device=dev)
+            gj = torch.empty((n_total, 16, 3), device=dev)
+            verts, joints = gv[a:b], gj[a:b]          # GPU 0's shard computed in place
+        else:
+            verts = torch.empty((Bl, V, 3), device=dev)
+            joints = torch.empty((Bl, 16, 3), device=dev)
+        if gather and nccl and gatherer is None:
+            wd.enter(f"leg_{name}:comm_create")
+            gatherer = AbiGather(local_dev)
+            wd.enter(f"leg_{name}")
+
+        def fwd():
+            if Bl:
+                model.forward(inp["betas"], inp["pose"], None, joints=True,
+                              out={"verts": verts, "joints": joints}, workspace=ws)
+
+        def gath():
+            if nccl:
+                gatherer.gather(verts, n_total, root=0, out=gv)
+                gatherer.gather(joints, n_total, root=0, out=gj)
+            else:
+                gather_rows_to_root(verts, n_total, out=gv, root=0, progress=note)
+                gather_rows_to_root(joints, n_total, out=gj, root=0)
+
+        host_gather = gather and not nccl
+        steps = 1 if host_gather else max(1, args.leg_steps)
+        if not host_gather:       # one untimed step (C4 on RCCL: RCCL sets up its channels)
+            fwd()
+            if gather:
+                gath()
+        torch.cuda.synchronize()
+        stream = torch.cuda.current_stream(dev)
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+        gather_host_s = []
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for e in evs:
+            e[0].record(stream)
+            fwd()
+            e[1].record(stream)
+            if gather:
+                if host_gather:
+                    torch.cuda.synchronize()
+                    tg = time.perf_counter()
+                    gath()
+                    torch.cuda.synchronize()
+                    gather_host_s.append(time.perf_counter() - tg)
+                else:
+                    gath()
+            e[2].record(stream)
+        torch.cuda.synchronize()
+        dist.barrier()
+        dt = time.perf_counter() - t0
+        t = torch.tensor([dt], device=red_dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        fwd_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+        res = {"desc": p["desc"], "global_batch": n_total, "baseline_size": p["baseline_size"], "seed": seed,
+               "ranks": world, "hands_per_rank": p["hands_per_rank"], "scaling": "strong",
+               "value": n_total * steps / dt, "unit": "hands/s", "per_gpu_hands_s": n_total * steps / dt / world,
+               "steps": steps, "ms_per_step": dt / steps * 1e3, "forward_ms_rank0": fwd_ms,
+               "forward_hands_s_rank0": Bl / (fwd_ms * 1e-3) if Bl and fwd_ms > 0 else None,
+               "path": "mano_forward (articulate + blend_skin16)" + (" + gather to GPU 0" if gather else ""),
+               "timing": "barrier + device sync on both sides of the timed steps, max over ranks; the leg is "
+                         "not part of the headline value"}
+        if gather:
+            per = -(-n_total // world)
+            if host_gather:
+                g = gather_stats("sendrecv", world, per, float(np.mean(gather_host_s)) * 1e3)
+                g.update({"backend": "gloo", "form": "gloo rehearsal: gather_rows_to_root through host memory "
+                                                     "in 32,768-row pieces (the mano_gather layout)",
+                          "timing": "host clock around the gather with device syncs (not an xGMI figure)"})
+            else:
+                gms = [e[1].elapsed_time(e[2]) for e in evs]
+                g = gather_stats("sendrecv", world, per, float(np.mean(gms)))
+                g.update({"backend": "nccl", "ms_min": float(np.min(gms)), "ms_max": float(np.max(gms)),
+                          "form": "mano_gather: one RCCL group of ncclSend (peers) / ncclRecv (GPU 0), each "
+                                  "peer over its own xGMI link; GPU 0's shard in place",
+                          "comm_ranks": gatherer.info()[0],
+                          "timing": "HIP events on rank 0's stream around the gather of each timed step"})
+            res["gather"] = g
+        # every rank's sampled hands of its shard vs the float64 oracle
+        wd.enter(f"leg_{name}:correctness")
+        chk = (check_sample(model, seed, a, Bl, inp["betas"], inp["pose"], None, verts, joints,
+                            args.model, False) if Bl else {"max_abs_err_verts": 0.0, "max_abs_err_joints": 0.0,
+                                                          "n_sampled": 0, "pass": True, "finite": True})
+        chk["device_status"] = model.device_status(clear=True)
+        chk["pass"] = bool(chk.get("pass")) and chk["device_status"] == 0
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, chk)
+        res["correctness"] = merge_checks(per_rank)
+        if gather and rank == 0:
+            ranges = [shard_range(n_total, r, world) for r in range(world)]
+            res["gather_check"] = check_gather(model, seed, None, world, gv, gj, False, ranges=ranges)
+        if gather and nccl and args.gather_compare_reps > 0 and n_total % world == 0:
+            # the ring all-gather of the same shards (SURVEY.md §5 / §8e: report both)
+            wd.enter(f"leg_{name}:allgather_compare")
+            av = torch.empty((n_total, V, 3), device=dev)
+            aj = torch.empty((n_total, 16, 3), device=dev)
+            gatherer.allgather(verts, out=av)
+            gatherer.allgather(joints, out=aj)
+            torch.cuda.synchronize()
+            dist.barrier()
+            cev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.gather_compare_reps)]
+            for e in cev:
+                e[0].record(stream)
+                gatherer.allgather(verts, out=av)
+                gatherer.allgather(joints, out=aj)
+                e[1].record(stream)
+            torch.cuda.synchronize()
+            cms = [e[0].elapsed_time(e[1]) for e in cev]
+            cmp_info = gather_stats("allgather", world, n_total // world, float(np.mean(cms)))
+            cmp_info.update({"ms_min": float(np.min(cms)), "ms_max": float(np.max(cms)), "reps": len(cms),
+                             "form": "mano_allgather: RCCL ring ncclAllGather, every rank receives the batch"})
+            if rank == 0:
+                ranges = [shard_range(n_total, r, world) for r in range(world)]
+                c = check_gather(model, seed, None, world, av, aj, False, ranges=ranges)
+                cmp_info["bit_exact"], cmp_info["hands_checked"] = c["bit_exact"], c["hands_checked"]
+            res["gather"]["compare"] = cmp_info
+            del av, aj
+            dist.barrier()
+        res["wall_s"] = round(time.monotonic() - t_leg, 3)
+        out[name] = res
+        del inp, ws, gv, gj, verts, joints
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    if gatherer is not None:
+        gatherer.close()
+    return out
 
 
 def load_traffic(path, kernel, batch):
@@ -588,7 +830,8 @@ def launch_check(args, wd):
     wd.cancel()
     if rank == 0:
         print(json.dumps({"launch_check": True, "n_gpus": world, "rank_sum": total,
-                          "local_ranks_ok": total == world * (world - 1) // 2}), flush=True)
+                          "local_ranks_ok": total == world * (world - 1) // 2,
+                          "legs": plan_legs(args, world)}), flush=True)
 
 
 def main(argv=None):
@@ -970,6 +1213,8 @@ def run(args, wd):
         gather_info["ms_max"] = float(np.max(gms))
         gather_info["sampled_steps"] = len(gms)
         gather_info["backend"] = args.backend
+        # the rank count RCCL's communicator holds (mano_comm_info), not the launcher's
+        gather_info["comm_ranks"] = gatherer.info()[0] if gatherer is not None else None
         gather_info["form"] = ({"sendrecv": "mano_gather: one RCCL group of ncclSend (peers) / ncclRecv "
                                             "(GPU 0), each peer over its own xGMI link",
                                 "allgather": "mano_allgather: RCCL ring ncclAllGather"}[impl]
@@ -1170,6 +1415,7 @@ def run(args, wd):
     # gather, GPU 0's assembled buffers vs a local forward of hands
     # regenerated by global index from every rank's range.
     correctness, gather_check = None, None
+    skipped = {}
     wd.enter("correctness")
     device_status = model.device_status(clear=True)  # MANO_DEVICE_* bits raised by any launch (0 = none)
     if not args.no_check:
@@ -1192,6 +1438,11 @@ def run(args, wd):
         if args.dump_gather:
             np.savez(args.dump_gather, verts=gv.cpu().numpy(), joints=gj.cpu().numpy())
 
+    # BASELINE's multi-GPU configs (C3, C4) as legs after the headline: every
+    # N > 1 run measures them (not part of `value`), inside the watchdog.
+    legs_plan = plan_legs(args, world) if dist_on else {}
+    legs = run_legs(args, legs_plan, model, rank, world, dev, local_dev, wd, skipped) if legs_plan else None
+
     # The collective phases are over.  Rank 0's host legs hold no collective
     # and each is bounded by its own child timeout, fitted into the deadline;
     # the other ranks wait for them at the gloo end barrier.  From here the
@@ -1203,7 +1454,7 @@ def run(args, wd):
     # Rank 0's host-side legs, at every N (the other ranks wait at a barrier,
     # their GPUs idle): roofline.traffic by two rocprofv3 --pmc passes over a
     # child run on rank 0's GPU only, the drop-in latency, the CPU baseline.
-    extra, skipped = {}, {}
+    extra = {}
     if rank == 0:
         if roof is not None:
             traffic, src, live = None, None, None
@@ -1305,6 +1556,8 @@ def run(args, wd):
             line["gather"] = gather_info
         if gather_check is not None:
             line["gather_check"] = gather_check
+        if legs is not None:
+            line["legs"] = legs
         line.update(extra)
         line["status"] = "ok"
         line["run"] = {"wall_s": round(time.monotonic() - T_START, 3), "phases": wd.phases,

@@ -277,6 +277,20 @@ int mano_gather(mano_comm* comm, const void* send, size_t send_bytes, void* recv
 int mano_comm_create_all(int32_t n, const int* devices, mano_comm** comms);
 int mano_group_start(void);
 int mano_group_end(void);
+/* Argument checks of one mano_gather call, without posting anything (ABI 7).
+ * A mano_gather that fails its checks posts nothing, but inside a group the
+ * calls BEFORE it have already posted theirs: ncclGroupEnd would launch a
+ * half-built group (a root receive with no matching send never completes),
+ * and RCCL has no way to abandon a group.  So a host that issues several
+ * gathers in one group checks every one of them with mano_gather_check
+ * first and calls mano_group_start only when all pass;
+ * mano_gather runs exactly these checks, so a call that passes here is not
+ * refused there.  (A HIP or RCCL failure after the checks -- a lost device --
+ * still leaves the group's streams undefined.) */
+int mano_gather_check(const mano_comm* comm, const void* send, size_t send_bytes,
+                      const void* recv, const size_t* rank_bytes, int32_t root);
+/* Size, rank and device of a communicator (each output nullable; ABI 7). */
+int mano_comm_info(const mano_comm* comm, int32_t* n_ranks, int32_t* rank, int32_t* device);
 /* Every rank receives every shard: RCCL's ring ncclAllGather of equal
  * `send_bytes` shards, rank r's bytes at recv + r * send_bytes on EVERY rank
  * (recv holds n_ranks * send_bytes; in place when send == recv + rank *
@@ -293,7 +307,7 @@ const char* mano_last_error(void);
 /* ABI version, bumped on any signature change (4: + mano_allgather; 5: +
  * mano_host_alloc / mano_host_free; 6: + mano_comm_create_all /
  * mano_group_start / mano_group_end, MANO_EDEVICE, mano_model_device_status
- * flags). */
+ * flags; 7: + mano_gather_check / mano_comm_info). */
 int mano_abi_version(void);
 
 #ifdef __cplusplus

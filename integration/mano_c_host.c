@@ -14,7 +14,7 @@
  * device its contiguous shard by global index), runs mano_forward on every
  * device from this one thread, assembles all verts + posed joints on device 0
  * with ONE RCCL group (mano_comm_create_all, mano_group_start, mano_gather per
- * device, mano_group_end; ABI 6) and writes them to out.bin as float32
+ * device (each checked first with mano_gather_check), mano_group_end; ABI 7) and writes them to out.bin as float32
  * [n][V][3] then [n][16][3].  Exit status 0 on success; every failing call's
  * mano_last_error() on stderr.
  */
@@ -55,8 +55,8 @@ int main(int argc, char** argv) {
     fprintf(stderr, "bad n_hands / n_devices\n");
     return 1;
   }
-  if (mano_abi_version() < 6) {
-    fprintf(stderr, "libmano_hip ABI %d < 6\n", mano_abi_version());
+  if (mano_abi_version() < 7) {
+    fprintf(stderr, "libmano_hip ABI %d < 7\n", mano_abi_version());
     return 2;
   }
 
@@ -130,6 +130,10 @@ int main(int argc, char** argv) {
   /* one RCCL group from this thread: every shard to device 0 */
   mano_comm** comms = calloc(n_dev, sizeof *comms);
   CHECK(mano_comm_create_all(n_dev, devices, comms));
+  /* every call of the group checked BEFORE the group posts anything (ABI 7):
+     a call refused half way would leave a root receive without its send */
+  for (int r = 0; r < n_dev; ++r) CHECK(mano_gather_check(comms[r], verts[r], vbytes[r], r == 0 ? all_v : NULL, vbytes, 0));
+  for (int r = 0; r < n_dev; ++r) CHECK(mano_gather_check(comms[r], joints[r], jbytes[r], r == 0 ? all_j : NULL, jbytes, 0));
   CHECK(mano_group_start());
   for (int r = 0; r < n_dev; ++r) CHECK(mano_gather(comms[r], verts[r], vbytes[r], r == 0 ? all_v : NULL, vbytes, 0, NULL));
   for (int r = 0; r < n_dev; ++r) CHECK(mano_gather(comms[r], joints[r], jbytes[r], r == 0 ? all_j : NULL, jbytes, 0, NULL));

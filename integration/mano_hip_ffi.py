@@ -34,7 +34,7 @@ LIB_PATH = os.environ.get(
 _p, _i32, _i64, _sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
 _d = ctypes.POINTER(ctypes.c_double)
 H2D, D2H = 1, 2  # MANO_MEMCPY_HOST_TO_DEVICE, MANO_MEMCPY_DEVICE_TO_HOST
-STATUS_NO_WAIT = 2  # MANO_STATUS_NO_WAIT
+STATUS_CLEAR, STATUS_NO_WAIT = 1, 2  # MANO_STATUS_CLEAR, MANO_STATUS_NO_WAIT
 N_JOINTS, N_SHAPE = 16, 10
 
 _lib = ctypes.CDLL(LIB_PATH)
@@ -177,11 +177,18 @@ class Engine:
 
     def _check_status(self):
         """The kernels finished: raise if one raised a MANO_DEVICE_* bit (its
-        outputs are not valid; include/mano_hip.h mano_model_device_status)."""
+        outputs are not valid; include/mano_hip.h mano_model_device_status).
+        The bits are taken (MANO_STATUS_CLEAR) when they are reported: the
+        error is raised once, for the call whose launches set them, and the
+        next forward launches again -- left set, every later launch on the
+        model would be refused with MANO_EDEVICE and the Engine unusable."""
         st = _i32(0)
         _check(_lib.mano_model_device_status(self._h, ctypes.byref(st), STATUS_NO_WAIT))
         if st.value:
-            raise RuntimeError(f"libmano_hip: device status 0x{st.value:x}: outputs not valid")
+            taken = _i32(0)
+            _check(_lib.mano_model_device_status(self._h, ctypes.byref(taken), STATUS_NO_WAIT | STATUS_CLEAR))
+            raise RuntimeError(f"libmano_hip: device status 0x{st.value | taken.value:x}: outputs not valid "
+                               "(status cleared)")
 
     def close(self):
         if self._h:

@@ -122,7 +122,7 @@ int set_error(int code, const char* msg) {
 
 extern "C" {
 
-int mano_abi_version(void) { return 6; }
+int mano_abi_version(void) { return 7; }
 
 const char* mano_last_error(void) { return g_last_error.c_str(); }
 

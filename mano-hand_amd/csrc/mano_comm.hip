@@ -252,23 +252,55 @@ int mano_comm_destroy(mano_comm* c) {
   return MANO_OK;
 }
 
-int mano_gather(mano_comm* c, const void* send, size_t send_bytes, void* recv,
-                const size_t* rank_bytes, int32_t root, void* stream) {
+int mano_comm_info(const mano_comm* c, int32_t* n_ranks, int32_t* rank, int32_t* device) {
   mano::set_error(MANO_OK, "");
+  if (int rc = check_comm(c)) return rc;
+  if (n_ranks) *n_ranks = c->n_ranks;
+  if (rank) *rank = c->rank;
+  if (device) *device = c->device;
+  return MANO_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Every check mano_gather makes before it touches a stream or posts an RCCL
+// op; `off` (root only) receives the per-rank landing offsets.  Shared by
+// mano_gather and mano_gather_check, so a call the pre-flight accepts is
+// never refused by the real one.
+int gather_args(const mano_comm* c, const void* send, size_t send_bytes, const void* recv,
+                const size_t* rank_bytes, int32_t root, std::vector<size_t>* off) {
   if (int rc = check_comm(c)) return rc;
   if (root < 0 || root >= c->n_ranks)
     return fail(MANO_EINVAL, "root %d out of range [0, %d)", root, c->n_ranks);
   if (send_bytes > 0 && !send) return fail(MANO_EINVAL, "send is NULL");
+  if (c->rank != root) return MANO_OK;
+  off->assign(c->n_ranks + 1, 0);
+  for (int p = 0; p < c->n_ranks; ++p) (*off)[p + 1] = (*off)[p] + (rank_bytes ? rank_bytes[p] : send_bytes);
+  if (rank_bytes && rank_bytes[root] != send_bytes)
+    return fail(MANO_EINVAL, "rank_bytes[root] = %zu but root sends %zu bytes", rank_bytes[root], send_bytes);
+  if ((*off)[c->n_ranks] > 0 && !recv) return fail(MANO_EINVAL, "recv is NULL on root");
+  return MANO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mano_gather_check(const mano_comm* c, const void* send, size_t send_bytes, const void* recv,
+                      const size_t* rank_bytes, int32_t root) {
+  mano::set_error(MANO_OK, "");
+  std::vector<size_t> off;
+  return gather_args(c, send, send_bytes, recv, rank_bytes, root, &off);
+}
+
+int mano_gather(mano_comm* c, const void* send, size_t send_bytes, void* recv,
+                const size_t* rank_bytes, int32_t root, void* stream) {
+  mano::set_error(MANO_OK, "");
+  std::vector<size_t> off;
+  if (int rc = gather_args(c, send, send_bytes, recv, rank_bytes, root, &off)) return rc;
   const bool is_root = c->rank == root;
-  std::vector<size_t> off(c->n_ranks + 1, 0);
-  if (is_root) {
-    for (int p = 0; p < c->n_ranks; ++p)
-      off[p + 1] = off[p] + (rank_bytes ? rank_bytes[p] : send_bytes);
-    if (rank_bytes && rank_bytes[root] != send_bytes)
-      return fail(MANO_EINVAL, "rank_bytes[root] = %zu but root sends %zu bytes", rank_bytes[root],
-                  send_bytes);
-    if (off[c->n_ranks] > 0 && !recv) return fail(MANO_EINVAL, "recv is NULL on root");
-  }
   const Rccl& r = rccl();
   DeviceGuard guard(c->device);
   if (guard.err != hipSuccess)

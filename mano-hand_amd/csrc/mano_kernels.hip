@@ -92,8 +92,11 @@ __device__ __forceinline__ void store_vposed_tile(float* __restrict__ vposed, co
                                                     0x00020000);
   // Every lane issues its 16 stores (the blend kernel's counted vmcnt needs
   // an exact per-wave count); a lane past the row end gets an offset beyond
-  // the buffer, whose store is dropped.
-  const int cbase = col < n_cols ? 4 * col : 0x7fff0000;
+  // the buffer, whose store is dropped.  The sentinel 2^30 is above any
+  // num_records here (lp <= 3: < 32 rows x 8 x 2,334 floats x 4 B = 2.4 MB)
+  // and leaves room for the row term (4 hr rstride < 2.4 MB), so the signed
+  // sum never overflows.
+  const int cbase = col < n_cols ? 4 * col : 0x40000000;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int hr = (r & 3) + 8 * (r >> 2) + 4 * hi;

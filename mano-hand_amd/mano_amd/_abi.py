@@ -20,7 +20,7 @@ MANO_COMM_ID_BYTES = 128
 MANO_PRECISION_FP32, MANO_PRECISION_F16X3 = 0, 1
 MANO_DEVICE_SKIN_HANDOFF_TIMEOUT = 1
 MANO_STATUS_CLEAR, MANO_STATUS_NO_WAIT = 1, 2
-ABI_VERSION = 6
+ABI_VERSION = 7
 PRECISIONS = {"fp32": MANO_PRECISION_FP32, "f16x3": MANO_PRECISION_F16X3}
 _CODE_NAMES = {MANO_EINVAL: "MANO_EINVAL", MANO_EHIP: "MANO_EHIP", MANO_ESMALL: "MANO_ESMALL",
                MANO_ESTATE: "MANO_ESTATE", MANO_ECOMM: "MANO_ECOMM", MANO_EDEVICE: "MANO_EDEVICE"}
@@ -98,6 +98,8 @@ SIGNATURES = {
     "mano_comm_destroy": (ctypes.c_int, [_p]),
     "mano_gather": (ctypes.c_int, [_p, _p, ctypes.c_size_t, _p, ctypes.POINTER(ctypes.c_size_t), _i32, _p]),
     "mano_allgather": (ctypes.c_int, [_p, _p, ctypes.c_size_t, _p, _p]),
+    "mano_gather_check": (ctypes.c_int, [_p, _p, ctypes.c_size_t, _p, ctypes.POINTER(ctypes.c_size_t), _i32]),
+    "mano_comm_info": (ctypes.c_int, [_p, ctypes.POINTER(_i32), ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
 }
 
 _LIB = None

@@ -65,6 +65,53 @@ def gather_to_root(shard: torch.Tensor, n_total: int, root: int = 0,
     return None
 
 
+def gather_rows_to_root(shard: torch.Tensor, n_total: int, out: Optional[torch.Tensor] = None,
+                        root: int = 0, chunk_rows: int = 32768, group=None,
+                        progress=None) -> Optional[torch.Tensor]:
+    """`gather_to_root` in bounded pieces, for a host-backend (gloo) group and
+    shards of many GB: every rank sends its shard in chunks of `chunk_rows`
+    rows through host memory (the last chunk zero-padded; every rank runs
+    the same ceil(ceil(n_total / world) / chunk_rows) collectives), and root
+    writes rank r's rows at shard_range(n_total, r)[0] + offset of `out` (any
+    device; allocated on the shard's device when None).  Host memory per
+    collective: world x chunk_rows rows on root, one chunk elsewhere.
+    `progress(rows_done, rows_per_rank)` is called after each chunk."""
+    world, rank = _world(group)
+    start, stop = shard_range(n_total, rank, world)
+    if shard.shape[0] != stop - start:
+        raise ValueError(f"rank {rank} shard has {shard.shape[0]} rows, expected {stop - start}")
+    if chunk_rows < 1:
+        raise ValueError("chunk_rows must be positive")
+    if rank == root and out is None:
+        out = shard.new_empty((n_total,) + tuple(shard.shape[1:]))
+    if world == 1:
+        if out.data_ptr() != shard.data_ptr():
+            out[start:stop].copy_(shard)
+        return out
+    dst = root if group is None else dist.get_global_rank(group, root)
+    per = -(-n_total // world)
+    ranges = [shard_range(n_total, r, world) for r in range(world)]
+    row_shape = tuple(shard.shape[1:])
+    for off in range(0, per, chunk_rows):
+        c = min(chunk_rows, per - off)
+        piece = torch.zeros((c,) + row_shape, dtype=shard.dtype)
+        have = max(0, min(c, shard.shape[0] - off))
+        if have:
+            piece[:have].copy_(shard[off:off + have])
+        if rank == root:
+            got = [torch.empty_like(piece) for _ in range(world)]
+            dist.gather(piece, gather_list=got, dst=dst, group=group)
+            for r, (a, b) in enumerate(ranges):
+                n = max(0, min(c, (b - a) - off))
+                if n and not (r == rank and out[a + off].data_ptr() == shard[off].data_ptr()):
+                    out[a + off:a + off + n].copy_(got[r][:n])
+        else:
+            dist.gather(piece, gather_list=None, dst=dst, group=group)
+        if progress is not None:
+            progress(off + c, per)
+    return out if rank == root else None
+
+
 def all_gather(shard: torch.Tensor, n_total: int, group=None) -> torch.Tensor:
     """Every rank receives the (n_total, ...) concatenation of all shards."""
     world, rank = _world(group)
@@ -98,6 +145,13 @@ class AbiGather:
             uid = ctypes.create_string_buffer(box[0], _abi.MANO_COMM_ID_BYTES)
         self._c = ctypes.c_void_p()
         _abi.check(lib.mano_comm_create(device, world, rank, uid, ctypes.byref(self._c)))
+
+    def info(self):
+        """(n_ranks, rank, device) as the RCCL communicator holds them
+        (mano_comm_info): what a multi-GPU run asserts RCCL actually saw."""
+        n, r, d = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        _abi.check(_abi.lib().mano_comm_info(self._c, ctypes.byref(n), ctypes.byref(r), ctypes.byref(d)))
+        return n.value, r.value, d.value
 
     def gather(self, shard: torch.Tensor, n_total: int, root: int = 0, out: Optional[torch.Tensor] = None,
                stream=None) -> Optional[torch.Tensor]:

@@ -54,19 +54,50 @@ class DeviceComms:
             raise RuntimeError("communicators are closed")
         lib = _abi.lib()
         n = len(self.devices)
+        if len(pieces) != n or len(streams) != n or not 0 <= root < n:
+            raise ValueError(f"{len(pieces)} piece lists / {len(streams)} streams / root {root} "
+                             f"for {n} devices")
+        # Every call's arguments, checked before the group posts anything
+        # (mano_gather_check runs mano_gather's own checks): a call refused
+        # half way through a group would leave the calls before it posted, and
+        # ncclGroupEnd would launch a root receive whose send never comes.
+        calls = []
+        for k, out in enumerate(outs):
+            if len(pieces[root]) <= k or out.device != pieces[root][k].device or not out.is_contiguous():
+                raise ValueError(f"output {k} must be contiguous on the root's device")
+            row = math.prod(out.shape[1:]) * out.element_size()
+            sizes = (ctypes.c_size_t * n)(*[pieces[i][k].shape[0] * row for i in range(n)])
+            if sum(sizes) != out.numel() * out.element_size():
+                raise ValueError(f"output {k} holds {out.shape[0]} rows, the pieces {sum(sizes) // row}")
+            for i in range(n):
+                p = pieces[i][k]
+                if not p.is_contiguous() or p.device != torch.device("cuda", self.devices[i]):
+                    raise ValueError(f"piece {k} of device {self.devices[i]} must be contiguous on it")
+                args = (self._c[i], ctypes.c_void_p(p.data_ptr()), p.shape[0] * row,
+                        ctypes.c_void_p(out.data_ptr()) if i == root else None, sizes, root)
+                _abi.check(lib.mano_gather_check(*args))
+                calls.append(args + (ctypes.c_void_p(streams[i].cuda_stream),))
         _abi.check(lib.mano_group_start())
         try:
-            for k, out in enumerate(outs):
-                row = math.prod(out.shape[1:]) * out.element_size()
-                sizes = (ctypes.c_size_t * n)(*[pieces[i][k].shape[0] * row for i in range(n)])
-                for i in range(n):
-                    p = pieces[i][k]
-                    _abi.check(lib.mano_gather(
-                        self._c[i], ctypes.c_void_p(p.data_ptr()), p.shape[0] * row,
-                        ctypes.c_void_p(out.data_ptr()) if i == root else None, sizes, root,
-                        ctypes.c_void_p(streams[i].cuda_stream)))
-        finally:
-            _abi.check(lib.mano_group_end())
+            for args in calls:
+                _abi.check(lib.mano_gather(*args))
+        except BaseException:
+            # a failure past the checks (HIP / RCCL): close the group without
+            # masking the original error; the streams' state is then undefined
+            lib.mano_group_end()
+            raise
+        _abi.check(lib.mano_group_end())
+
+    def n_ranks(self) -> List[int]:
+        """Each communicator's rank count as RCCL holds it (mano_comm_info)."""
+        if self._c is None:
+            raise RuntimeError("communicators are closed")
+        out = []
+        for c in self._c:
+            n = ctypes.c_int32()
+            _abi.check(_abi.lib().mano_comm_info(c, ctypes.byref(n), None, None))
+            out.append(n.value)
+        return out
 
     def close(self):
         if self._c is not None:
@@ -111,6 +142,17 @@ class ManoMultiDevice:
         return self._comms
 
     # ---------------------------------------------------------------- forward
+    def _enter(self):
+        """Order this call's work after everything the caller has queued on
+        each device's current stream.  The returned tensors are allocated on
+        the internal streams, so when the caller frees one, the caching
+        allocator may hand its block to the next call's allocations on those
+        streams at once; with the internal streams waiting here, the next
+        call's writes cannot overtake the caller's reads of the old result
+        (nor its writes of this call's inputs)."""
+        for d, s in zip(self.devices, self.streams):
+            s.wait_stream(torch.cuda.current_stream(torch.device("cuda", d)))
+
     def _alloc_outputs(self, n_total, joints, gather):
         """Per device: the (verts, joints) its forward writes.  With a gather,
         the root's rows of the assembled buffers (allocated on the root's
@@ -181,6 +223,7 @@ class ManoMultiDevice:
         gather = gather or False
         B = pose.shape[0]
         pose = pose.reshape(B, N_JOINTS, 3)
+        self._enter()
         ranges, per, assembled = self._alloc_outputs(B, joints, gather)
         src_stream = torch.cuda.current_stream(pose.device) if pose.is_cuda else None
         for i, (eng, d, s) in enumerate(zip(self.engines, self.devices, self.streams)):
@@ -209,6 +252,7 @@ class ManoMultiDevice:
         B = pca.shape[0] if pca.dim() == 2 else (betas.shape[0] if betas.dim() == 2 else None)
         if B is None:
             raise ValueError("batch size unknown: give (B,N) pca or (B,10) betas")
+        self._enter()
         ranges, per, assembled = self._alloc_outputs(B, joints, gather)
         src = next((t for t in (pca, betas, rot, trans) if t is not None and t.is_cuda), None)
         src_stream = torch.cuda.current_stream(src.device) if src is not None else None
@@ -237,6 +281,7 @@ class ManoMultiDevice:
         if gather not in ("rccl", "copy", False, None):
             raise ValueError(f"gather must be 'rccl', 'copy' or False, got {gather!r}")
         gather = gather or False
+        self._enter()
         ranges, per, assembled = self._alloc_outputs(n_total, joints, gather)
         for i, (eng, s) in enumerate(zip(self.engines, self.streams)):
             a, b = ranges[i]
@@ -245,6 +290,45 @@ class ManoMultiDevice:
             inp = eng.synthetic_inputs(seed, a, b - a, trans=trans, stream=s)  # allocated on s
             eng.forward(inp["betas"], inp["pose"], inp.get("trans"), joints=joints, out=per[i], stream=s)
         return self._finish(ranges, per, assembled, joints, gather)
+
+    def gather_bandwidth(self, n_total: int, reps: int = 5, seed: int = 1003) -> Dict[str, object]:
+        """Measure the RCCL group gather alone: every device forwards its shard
+        of `n_total` synthetic hands (the root's in place in the assembled
+        buffers), then the gather of verts + joints into the root runs `reps`
+        times between HIP events on the root's stream (after one untimed
+        call).  Returns the mean ms and the rate of the peers' bytes into the
+        root -- the xGMI figure of a multi-GPU node."""
+        self._enter()
+        ranges, per, assembled = self._alloc_outputs(n_total, True, True)
+        for i, (eng, s) in enumerate(zip(self.engines, self.streams)):
+            a, b = ranges[i]
+            if b > a:
+                inp = eng.synthetic_inputs(seed, a, b - a, stream=s)
+                eng.forward(inp["betas"], inp["pose"], None, joints=True, out=per[i], stream=s)
+        keys = ("verts", "joints")
+        pieces = [[p[k] for k in keys] for p in per]
+        outs = [assembled[k] for k in keys]
+        comms = self.comms()
+        comms.gather(pieces, outs, self.root, self.streams)
+        for d in sorted(set(self.devices)):
+            torch.cuda.synchronize(d)
+        rs = self.streams[self.root]
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for e0, e1 in evs:
+            for d in sorted(set(self.devices)):
+                torch.cuda.synchronize(d)
+            e0.record(rs)
+            comms.gather(pieces, outs, self.root, self.streams)
+            e1.record(rs)
+        for d in sorted(set(self.devices)):
+            torch.cuda.synchronize(d)
+        ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / max(1, reps)
+        row = sum(math.prod(o.shape[1:]) * o.element_size() for o in outs)
+        to_root = sum((b - a) * row for i, (a, b) in enumerate(ranges) if i != self.root)
+        return {"ms": ms, "bytes_to_root": to_root, "GBs_to_root": to_root / (ms * 1e-3) / 1e9 if ms > 0 else None,
+                "devices": list(self.devices), "reps": reps,
+                "form": "one RCCL group of mano_gather from this thread (peers' ncclSend, the root's "
+                        "ncclRecv), the root's shard in place; HIP events on the root's stream"}
 
     def synchronize(self) -> None:
         """Wait for every device's stream; raise DeviceStatusError if a launch

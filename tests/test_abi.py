@@ -17,7 +17,7 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, n), n
         assert n in _abi.SIGNATURES, f"{n} declared in the header but not bound"
     assert set(_abi.SIGNATURES) == set(names)
-    assert lib.mano_abi_version() == _abi.ABI_VERSION == 6
+    assert lib.mano_abi_version() == _abi.ABI_VERSION == 7
 
 
 @pytest.mark.parametrize("cc,lang", [("g++", "c++"), ("gcc", "c")])
@@ -108,6 +108,10 @@ def test_forward_pca_and_comm_argument_checks():
     assert lib.mano_gather(None, None, 0, None, None, 0, None) == _abi.MANO_EINVAL
     assert lib.mano_allgather(None, None, 0, None, None) == _abi.MANO_EINVAL
     assert lib.mano_comm_unique_id(None) == _abi.MANO_EINVAL
+    # ABI 7: the pre-flight check and the info query refuse a NULL comm too
+    assert lib.mano_gather_check(None, None, 0, None, None, 0) == _abi.MANO_EINVAL
+    n = ctypes.c_int32(-7)
+    assert lib.mano_comm_info(None, ctypes.byref(n), None, None) == _abi.MANO_EINVAL and n.value == -7
 
 
 def test_makefile_matches_build_flags():

@@ -32,6 +32,43 @@ def test_gpus_flag_launches_n_ranks(n):
     assert line["n_gpus"] == n and line["local_ranks_ok"]
 
 
+@pytest.mark.parametrize("n", [2, 8])
+def test_launch_check_plans_the_multi_gpu_legs(n):
+    """Every N > 1 run measures BASELINE's multi-GPU configs after the C2
+    headline: the launch path (torchrun, gloo, no GPU) reports the legs each
+    rank will run -- C3's 2^24 hands and C4's 2^22 hands split over the N
+    ranks (strong scaling, the BASELINE sizes), C4 with the gather to GPU 0."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(n),
+                        "--backend", "gloo", "--launch-check"], capture_output=True, text=True,
+                       timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    legs = _last_json(r.stdout)["legs"]
+    assert set(legs) == {"C3", "C4"}
+    c3, c4 = legs["C3"], legs["C4"]
+    assert c3["global_batch"] == 2 ** 24 and c3["seed"] == 1002 and not c3["gather_to_gpu0"]
+    assert c4["global_batch"] == 2 ** 22 and c4["seed"] == 1003 and c4["gather_to_gpu0"]
+    for leg in (c3, c4):
+        assert leg["baseline_size"] and leg["scaling"] == "strong"
+        assert leg["hands_per_rank"] == [leg["global_batch"] // n] * n
+    if n == 8:   # SURVEY.md §8 per-GPU sizes
+        assert c3["hands_per_rank"][0] == 2097152 and c4["hands_per_rank"][0] == 524288
+
+
+def test_legs_plan_flags():
+    """One rank: no legs unless asked; --leg-global resizes a leg (and says
+    so); ragged splits keep every hand."""
+    assert bench.plan_legs(bench.parse([]), 1) == {}
+    assert bench.plan_legs(bench.parse(["--legs", "off"]), 8) == {}
+    p = bench.plan_legs(bench.parse(["--legs", "on", "--leg-global", "C3=1003,C4=64"]), 3)
+    assert p["C3"]["global_batch"] == 1003 and not p["C3"]["baseline_size"]
+    assert sum(p["C3"]["hands_per_rank"]) == 1003 and sum(p["C4"]["hands_per_rank"]) == 64
+    with pytest.raises(SystemExit):
+        bench.parse_leg_global("C9=4")
+    a = bench.parse([])
+    assert a.leg_min_seconds < a.watchdog_seconds and a.leg_steps >= 1
+
+
 def test_failure_budgets_inside_driver_lease():
     """The driver kills a bench run at 600 s: a stalled collective must raise
     (process-group timeout) before the watchdog fires, the watchdog before the

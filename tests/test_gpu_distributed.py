@@ -219,7 +219,8 @@ def test_bench_two_gpus_nccl_gather(impl):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "nccl",
            "--workload", "C4", "--batch", str(B), "--steps", "5", "--warmup", "2", "--ramp-seconds", "0",
-           "--gather-impl", impl, "--no-extra", "--no-dropin", "--no-cpu", "--no-live-pmc"]
+           "--gather-impl", impl, "--no-extra", "--no-dropin", "--no-cpu", "--no-live-pmc",
+           "--leg-global", "C3=131072,C4=65536"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
@@ -227,11 +228,17 @@ def test_bench_two_gpus_nccl_gather(impl):
     assert line["gather_check"]["bit_exact"] and line["gather_check"]["ranks"] == 2, line["gather_check"]
     assert line["correctness"]["pass"] and line["correctness"]["ranks_checked"] == 2, line["correctness"]
     g = line["gather"]
-    assert g["impl"] == impl and g["ms"] > 0
+    assert g["impl"] == impl and g["ms"] > 0 and g["comm_ranks"] == 2   # RCCL saw both ranks
     assert g["bytes_to_gpu0"] == B * (778 * 3 + 16 * 3) * 4
     assert g["GBs_to_gpu0"] > 0 and g["link_frac"] is not None
     c = g["compare"]
     assert c["bit_exact"] and c["ms"] > 0
+    # the multi-GPU legs ran too (smaller than BASELINE's: --leg-global)
+    legs = line["legs"]
+    assert legs["C3"]["correctness"]["pass"] and legs["C3"]["correctness"]["ranks_checked"] == 2
+    lg = legs["C4"]["gather"]
+    assert lg["backend"] == "nccl" and lg["comm_ranks"] == 2 and lg["GBs_to_gpu0"] > 0
+    assert legs["C4"]["gather_check"]["bit_exact"] and lg["compare"]["bit_exact"]
 
 
 @pytest.mark.skipif(_visible_gpus() < 2, reason="the RCCL gather across ranks needs 2 GPUs")
@@ -324,3 +331,53 @@ def test_bench_deadline_skips_rank0_legs():
     assert line["roofline"]["traffic"] is not None            # the committed PMC summary stands in
     assert "skipped" in line["roofline"]["traffic_source"]
     assert line["run"]["wall_s"] < 60
+
+
+def _legs_run(extra, timeout=400):
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--batch", "4096", "--steps", "5",
+                        "--warmup", "1", "--ramp-seconds", "0", "--no-cpu", "--no-extra", "--no-dropin",
+                        "--no-live-pmc", *extra], capture_output=True, text=True, timeout=timeout, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+
+
+def _check_legs(legs, world, sizes):
+    assert set(legs) == {"C3", "C4"}
+    for name, n in sizes.items():
+        leg = legs[name]
+        assert leg["global_batch"] == n and not leg["baseline_size"] and leg["scaling"] == "strong"
+        assert sum(leg["hands_per_rank"]) == n and leg["ranks"] == world
+        assert leg["value"] > 0 and leg["ms_per_step"] > 0 and leg["forward_ms_rank0"] > 0
+        c = leg["correctness"]
+        assert c["pass"] and c["ranks_checked"] == world and c["max_abs_err_verts"] <= 1e-5, c
+    assert "gather" not in legs["C3"]
+    g = legs["C4"]["gather"]
+    assert legs["C4"]["gather_check"]["bit_exact"], legs["C4"]["gather_check"]
+    assert legs["C4"]["gather_check"]["ranks"] == world
+    return g
+
+
+def test_bench_legs_gloo_two_ranks():
+    """The legs of an N > 1 run, rehearsed with 2 gloo ranks sharing the GPU:
+    C3 and C4 at ragged sizes (1,003-hand-odd splits), every rank's sampled
+    hands vs the oracle, and C4's gather of both ranks' verts + joints into
+    GPU 0's contiguous buffers through host memory in pieces -- bit-exact
+    against hands regenerated by global index."""
+    line = _legs_run(["--gpus", "2", "--backend", "gloo", "--leg-global", "C3=40003,C4=20001"])
+    assert line["status"] == "ok" and line["n_gpus"] == 2
+    g = _check_legs(line["legs"], 2, {"C3": 40003, "C4": 20001})
+    assert g["backend"] == "gloo" and g["ms"] > 0 and g["bytes_to_gpu0"] > 0
+
+
+def test_bench_legs_one_rank_nccl():
+    """The RCCL form of the legs at one rank (--force-pg): C4's mano_gather
+    (GPU 0's shard in place), the communicator reporting 1 rank, and the ring
+    all-gather comparison bit-exact."""
+    line = _legs_run(["--force-pg", "--backend", "nccl", "--legs", "on", "--leg-global", "C3=131072,C4=65536"])
+    assert line["process_group"]["backend"] == "nccl"
+    g = _check_legs(line["legs"], 1, {"C3": 131072, "C4": 65536})
+    assert g["backend"] == "nccl" and g["comm_ranks"] == 1 and g["bytes_to_gpu0"] == 0
+    assert g["compare"]["bit_exact"] and g["compare"]["ms"] > 0

@@ -1,5 +1,6 @@
 """The single-process multi-GPU path (mano_amd.multi_device, include/mano_hip.h
-ABI 6: mano_comm_create_all + mano_group_start / mano_group_end).
+ABI 6: mano_comm_create_all + mano_group_start / mano_group_end; ABI 7:
+mano_gather_check, the pre-flight of a group's calls).
 
 One host thread drives every device: shards of one batch run on their own
 GPUs and streams, and the assembled outputs on the root equal the
@@ -71,6 +72,127 @@ def test_abi_group_gather_not_in_place():
         assert torch.equal(dst[:src.numel()], src) and not dst[src.numel():].any()
     finally:
         _abi.check(lib.mano_comm_destroy(ctypes.c_void_p(comms[0])))
+
+
+def _completes(stream, seconds=60.0):
+    """True when everything queued on `stream` so far finishes within
+    `seconds` (an event polled from the host: a hung group fails the test
+    instead of hanging it)."""
+    import time
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    t_end = time.monotonic() + seconds
+    while not ev.query():
+        if time.monotonic() > t_end:
+            return False
+        time.sleep(0.005)
+    return True
+
+
+def test_abi_group_preflight_refuses_second_call_before_anything_posts():
+    """ABI 7's rule for a group of gathers (the partial-group hang): the host
+    checks EVERY call with mano_gather_check before mano_group_start.  Here
+    the second call of the group is bad (rank_bytes[root] != send_bytes, then
+    root out of range, then recv NULL on the root): the check returns
+    MANO_EINVAL, the host never opens the group, and nothing is launched --
+    the first call's out-of-place destination is untouched.  The good group
+    that follows completes within a timeout and lands its bytes."""
+    from mano_amd import _abi
+    lib = _abi.lib()
+    comms = (ctypes.c_void_p * 1)()
+    _abi.check(lib.mano_comm_create_all(1, (ctypes.c_int * 1)(0), comms))
+    c = ctypes.c_void_p(comms[0])
+    try:
+        n = ctypes.c_int32()
+        _abi.check(lib.mano_comm_info(c, ctypes.byref(n), None, None))
+        assert n.value == 1
+        s = torch.cuda.current_stream(0)
+        src_v = torch.arange(4096, dtype=torch.float32, device="cuda:0")
+        src_j = torch.arange(256, dtype=torch.float32, device="cuda:0") + 0.5
+        dst_v = torch.full((4096,), -7.0, device="cuda:0")
+        dst_j = torch.full((256,), -7.0, device="cuda:0")
+        torch.cuda.synchronize()
+        vb, jb = (ctypes.c_size_t * 1)(4096 * 4), (ctypes.c_size_t * 1)(256 * 4)
+        first = (c, ctypes.c_void_p(src_v.data_ptr()), 4096 * 4, ctypes.c_void_p(dst_v.data_ptr()), vb, 0)
+        assert lib.mano_gather_check(*first) == _abi.MANO_OK
+        bad_calls = [
+            (c, ctypes.c_void_p(src_j.data_ptr()), 256 * 4, ctypes.c_void_p(dst_j.data_ptr()), vb, 0),
+            (c, ctypes.c_void_p(src_j.data_ptr()), 256 * 4, ctypes.c_void_p(dst_j.data_ptr()), jb, 1),
+            (c, ctypes.c_void_p(src_j.data_ptr()), 256 * 4, None, jb, 0),
+        ]
+        for bad in bad_calls:
+            assert lib.mano_gather_check(*bad) == _abi.MANO_EINVAL
+            assert _abi.last_error()
+            # mano_gather runs the same checks and posts nothing either
+            assert lib.mano_gather(*bad, ctypes.c_void_p(s.cuda_stream)) == _abi.MANO_EINVAL
+        assert _completes(s)
+        assert bool((dst_v == -7.0).all()) and bool((dst_j == -7.0).all())   # nothing launched
+        good = (c, ctypes.c_void_p(src_j.data_ptr()), 256 * 4, ctypes.c_void_p(dst_j.data_ptr()), jb, 0)
+        assert lib.mano_gather_check(*good) == _abi.MANO_OK
+        _abi.check(lib.mano_group_start())
+        _abi.check(lib.mano_gather(*first, ctypes.c_void_p(s.cuda_stream)))
+        _abi.check(lib.mano_gather(*good, ctypes.c_void_p(s.cuda_stream)))
+        _abi.check(lib.mano_group_end())
+        assert _completes(s)
+        assert torch.equal(dst_v, src_v) and torch.equal(dst_j, src_j)
+    finally:
+        _abi.check(lib.mano_comm_destroy(c))
+
+
+def test_device_comms_bad_second_output_launches_nothing(params):
+    """DeviceComms.gather validates every call of its group before the group
+    opens: a bad SECOND output (its row count does not match the pieces)
+    raises, the first output's out-of-place destination is untouched, and a
+    following good gather completes within a timeout, bit for bit."""
+    from mano_amd import DeviceComms
+    d = torch.device("cuda", 0)
+    v = torch.randn(100, 778, 3, device=d)
+    j = torch.randn(100, 16, 3, device=d)
+    out_v = torch.full((100, 778, 3), -3.0, device=d)
+    bad_j = torch.full((99, 16, 3), -3.0, device=d)
+    s = torch.cuda.current_stream(0)
+    dc = DeviceComms([0])
+    try:
+        assert dc.n_ranks() == [1]
+        torch.cuda.synchronize()
+        with pytest.raises(ValueError):
+            dc.gather([[v, j]], [out_v, bad_j], 0, [s])
+        assert _completes(s)
+        assert bool((out_v == -3.0).all()) and bool((bad_j == -3.0).all())
+        out_j = torch.empty(100, 16, 3, device=d)
+        dc.gather([[v, j]], [out_v, out_j], 0, [s])
+        assert _completes(s)
+        assert torch.equal(out_v, v) and torch.equal(out_j, j)
+    finally:
+        dc.close()
+
+
+def test_results_safe_to_free_on_the_callers_stream(params):
+    """The returned tensors live on ManoMultiDevice's internal streams: a
+    result read on the caller's stream, freed, then the next forward_synthetic
+    (whose allocations may reuse its block) must not overwrite it mid-read --
+    each call orders its streams after the caller's.  A slow read of the
+    first result (a long copy chain on the current stream) still sees its
+    values."""
+    from mano_amd import ManoMultiDevice
+    n, seed = 4096, 1002
+    ref, _ = _reference(params, seed, n, trans=False)
+    other, _ = _reference(params, seed + 1, n, trans=False)
+    md = ManoMultiDevice(params, devices=[0])
+    try:
+        out = md.forward_synthetic(seed, n, gather=False)[0]
+        cur = torch.cuda.current_stream(0)
+        acc = torch.zeros_like(out["verts"])
+        for _ in range(200):            # a long read of the result on the caller's stream
+            acc.copy_(out["verts"])
+        del out                          # freed while the reads are still queued
+        nxt = md.forward_synthetic(seed + 1, n, gather=False)[0]
+        cur.wait_stream(md.streams[0])
+        torch.cuda.synchronize()
+        assert torch.equal(acc.cpu(), ref["verts"])
+        assert torch.equal(nxt["verts"].cpu(), other["verts"])
+    finally:
+        md.close()
 
 
 def test_duplicate_device_refused_by_rccl_form():
@@ -173,6 +295,13 @@ def test_two_devices_rccl_group_gather(params):
         out = md.forward_synthetic(seed, n, trans=True, gather="rccl")
         md.synchronize()
         assert torch.equal(out["verts"].cpu(), ref["verts"]) and torch.equal(out["joints"].cpu(), ref["joints"])
+        assert md.comms().n_ranks() == [2, 2]      # RCCL's communicators hold both devices
+        # the first xGMI figure: device 1's shard of a C4-sized batch into device 0
+        import warnings
+        gb = md.gather_bandwidth(2 * 262144)
+        assert gb["GBs_to_root"] > 0 and gb["bytes_to_root"] > 0
+        warnings.warn(f"xGMI gather device 1 -> 0 (one RCCL group, ManoMultiDevice): "
+                      f"{gb['GBs_to_root']:.1f} GB/s, {gb['bytes_to_root'] / 1e9:.2f} GB in {gb['ms']:.3f} ms")
     finally:
         md.close()
 

@@ -1,0 +1,35 @@
+#!/bin/bash
+# Round 6 GPU steps, each time-limited; stop on the first fault / timeout.
+#   STEPS="tests bench dp8" TAG=r06a bash tools/gpu_r06.sh
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${TAG:-r06}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" | tee -a $OUT/steps.log
+  local t0=$(date +%s%N)
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  local t1=$(date +%s%N)
+  echo "=== $name rc=$rc wall_ms=$(( (t1 - t0) / 1000000 ))" | tee -a $OUT/steps.log
+  tail -3 "$OUT/$name.log" | cut -c1-600
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after rc=$rc"; exit $rc; fi
+  if [ $rc -eq 1 ] && [ "${STOP_ON_FAIL:-1}" = 1 ]; then echo "stopping after rc=1"; exit 1; fi
+  return 0
+}
+for s in ${STEPS:-tests bench}; do
+  case $s in
+    tests) step pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread ${PYTEST_ARGS:-} ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 500 python bench.py --steps 20 --warmup 5 ;;
+    # the driver's N = 8 command, rehearsed with 8 gloo ranks sharing this
+    # box's one GPU, every rank-0 leg on (the CPU baseline at the box's
+    # 16-core share instead of cpu_share(8) = 128)
+    dp8) step bench_dp8 600 python bench.py --gpus 8 --backend gloo --steps 20 --warmup 5 --cpu-procs 16 ;;
+    stats) step stats 500 rocprofv3 --kernel-trace --stats -d $OUT/stats -o bench --output-format csv -- python bench.py --no-cpu ;;
+    *) step extra_$s 600 bash -c "$s" ;;
+  esac
+done
