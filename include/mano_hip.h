@@ -159,7 +159,12 @@ int mano_forward(const mano_model* model, int64_t n_hands,
  *              pose features (:87-91) + kinematic chain (:96-104) +
  *              rest-pose removal (:106-110).
  *  blend:      v_posed = T + S.beta + P.features (:81, :87-93) on MFMA.
- *  skin:       LBS (:112-115), + trans. */
+ *  skin:       LBS (:112-115), + trans.  rest_verts (NULL = the workspace's
+ *              v_posed) may be verts itself: the LBS then runs in place
+ *              (ABI 7; the blend writes v_posed into verts, the LBS
+ *              overwrites it -- no second buffer, and its writes land on the
+ *              blend's still-cached lines); any other overlap of the two is
+ *              MANO_EINVAL. */
 int mano_stage_articulate(const mano_model* model, int64_t n_hands,
                           const float* betas, int64_t betas_stride,
                           const float* pose, const float* trans, float* joints,
@@ -307,7 +312,7 @@ const char* mano_last_error(void);
 /* ABI version, bumped on any signature change (4: + mano_allgather; 5: +
  * mano_host_alloc / mano_host_free; 6: + mano_comm_create_all /
  * mano_group_start / mano_group_end, MANO_EDEVICE, mano_model_device_status
- * flags; 7: + mano_gather_check / mano_comm_info). */
+ * flags; 7: + mano_gather_check / mano_comm_info, in-place mano_stage_skin). */
 int mano_abi_version(void);
 
 #ifdef __cplusplus

@@ -384,11 +384,34 @@ int mano_stage_skin(const mano_model* m, int64_t n, const float* rest_verts, con
   if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
   const mano::Workspace w = mano::workspace_layout(m->dm, n);
   char* base = static_cast<char*>(ws);
-  const float* vp = rest_verts ? rest_verts : reinterpret_cast<const float*>(base + w.vposed_off);
-  auto launch = m->dm.precision == MANO_PRECISION_F16X3 ? mano::launch_skin_h3 : mano::launch_skin;
-  hipError_t e =
-      launch(m->dm, n, reinterpret_cast<const float*>(base + w.transforms_off), vp,
-                        trans, verts, static_cast<hipStream_t>(stream));
+  float* ws_vp = reinterpret_cast<float*>(base + w.vposed_off);
+  const float* vp = rest_verts ? rest_verts : ws_vp;
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  const float* tr = reinterpret_cast<const float*>(base + w.transforms_off);
+  // verts == rest_verts: the LBS in place over its own input (the unfused
+  // path's blend GEMM writes v_posed straight into verts).  Any other
+  // overlap of the two row ranges has no defined result.
+  const size_t bytes = size_t(n) * 3 * size_t(m->dm.n_verts) * sizeof(float);
+  const char *src = reinterpret_cast<const char*>(vp), *dst = reinterpret_cast<const char*>(verts);
+  const bool in_place = src == dst;
+  if (!in_place && src < dst + bytes && dst < src + bytes)
+    return fail(MANO_EINVAL, "verts and rest_verts overlap without being the same rows");
+  hipError_t e;
+  if (in_place && m->dm.precision == MANO_PRECISION_FP32 && mano::skin_in_place_supported(m->dm, n)) {
+    e = mano::launch_skin_quad(m->dm, n, tr, vp, trans, verts, s, false, true);
+  } else {
+    if (in_place) {
+      // no in-place kernel for this call (f16x3, a batch below one skin_pair
+      // block, a mesh skin_pair does not take): the rows go to the
+      // workspace's v_posed first, then the out-of-place LBS
+      if (verts == ws_vp) return fail(MANO_EINVAL, "verts is the workspace's own v_posed");
+      e = hipMemcpyAsync(ws_vp, vp, bytes, hipMemcpyDeviceToDevice, s);
+      if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync");
+      vp = ws_vp;
+    }
+    e = m->dm.precision == MANO_PRECISION_F16X3 ? mano::launch_skin_h3(m->dm, n, tr, vp, trans, verts, s)
+                                                 : mano::launch_skin(m->dm, n, tr, vp, trans, verts, s);
+  }
   if (e != hipSuccess) return hip_fail(e, "skin launch");
   return MANO_OK;
 }

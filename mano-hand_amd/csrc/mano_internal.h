@@ -90,9 +90,13 @@ hipError_t launch_skin(const DeviceModel& m, int64_t n, const float* transforms,
 // The 4-hand-unit fp32 LBS (mano_skin_quad.hip); launch_skin uses it when
 // skin_quad_supported(m) (16 <= V <= 832: W of every group resident in LDS).
 bool skin_quad_supported(const DeviceModel& m);
+// `in_place` (verts == vposed): skin_pair's in-place fp32 units, when
+// skin_in_place_supported(m, n); otherwise hipErrorNotSupported (the caller
+// then stages the rows elsewhere first).
+bool skin_in_place_supported(const DeviceModel& m, int64_t n);
 hipError_t launch_skin_quad(const DeviceModel& m, int64_t n, const float* transforms,
                             const float* vposed, const float* trans, float* verts,
-                            hipStream_t stream, bool h3 = false);
+                            hipStream_t stream, bool h3 = false, bool in_place = false);
 // f16x3 mode (mano_kernels_h3.hip): same operands and outputs as
 // launch_blend_skin (verts only: no v_posed output) / launch_skin.
 hipError_t launch_blend_skin_h3(const DeviceModel& m, int64_t n, const float* features,

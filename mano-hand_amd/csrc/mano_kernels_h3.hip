@@ -37,6 +37,23 @@
 // rest_verts runs the exact-fp32 blend_skin16 (mano_abi.hip), so f16x3
 // arithmetic is used for verts-only forwards.  The guards stay (no_pack,
 // -fno-slp-vectorize, the ISA scans of tests/test_codegen.py).
+//
+// CORRECTNESS DEPENDS ON THE BUILD FLAG.  The kernels that remain are correct
+// as built with -fno-slp-vectorize (no packed fp32 anywhere in the library);
+// the root cause of the packed-FMA miscompute was never found, so nothing
+// says the remaining kernels would stay correct if the vectorizer paired
+// their scalars again.  Two CPU tests guard it: the flag is on both build
+// recipes (test_no_slp_vectorize_flag_on_every_build) and the disassembly
+// has no v_pk_*_f32 (test_no_packed_fp32_valu).
+//
+// FROZEN (round 6).  The mode is opt-in and off the headline: blend_skin_h3
+// runs at 0.263 ms = 33 % of 8 TB/s on its 10,744 B/hand (2.67 TB/s, 18 %
+// more counter traffic than algorithmic), the sum of a latency-bound GEMM
+// phase and a store phase that do not overlap.  The one split left that
+// could overlap them (a wave per output coordinate or vertex group with its
+// B fragments in registers) was priced by its store order alone at 0.210 ms
+// for the stores (profiles/r05/r05w_store_patterns.txt) -- above the 0.20-ms
+// mark a rebuild would need -- so no further variant is built.
 #include "mano_internal.h"
 #include "mano_span.h"
 

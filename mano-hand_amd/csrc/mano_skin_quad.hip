@@ -520,6 +520,7 @@ __device__ __forceinline__ void pair_signal(int* flag, int value) {
 }
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
 // LDS-DMA buffer loads (device-only helpers: the host pass of a kernel
 // template cannot instantiate this builtin and would silently drop the stub).
@@ -594,13 +595,35 @@ struct PairStamp {
 // float4 per row, lanes 0-11 and 12-23 of one DMA) and skins them as two
 // groups -- the rows' first and last sectors, which neighbouring hands share
 // in any layout, and the aligned spans' edges rewritten with identical values.
-template <bool kTrans, bool kH3 = false, bool kAlign = false>
+//
+// kInPlace (fp32, plain units): verts == vposed, the LBS overwrites its own
+// input (the unfused path's blend GEMM writes v_posed into the verts buffer).
+// Units are disjoint except the tail: its segment starts d = 64 n_full -
+// tail_v0 vertices inside the last full span (V = 778: d = 6), whose unit
+// owns them.  So the tail unit stores only its own rows' floats ov = 3 d ..:
+// whole float4 past ov, and the float4 straddling ov as a b32 (dword 1 or 3)
+// plus a b64 (dwords 2-3) from its sweep-0 lane -- every unit issues those two
+// extra stores (dropped: an offset past num_records), so the step's
+// vector-memory op count stays fixed.  The tail's reads of the d shared
+// vertices may then see the span's skinned values; they feed only the d
+// outputs it does not store.  Hand quads go last-first: the blend GEMM's last
+// ~256 MB of v_posed are still dirty in the Infinity Cache when the LBS
+// starts, so their reads hit and their lines are overwritten in the cache
+// instead of being written back first.
+#ifndef MANO_PAIR_INPLACE_FORWARD
+#define MANO_PAIR_INPLACE_FORWARD 0  // diagnostic builds: 1 = in-place units in hand order
+#endif
+#ifndef MANO_PAIR_INPLACE_ORDER
+#define MANO_PAIR_INPLACE_ORDER 0  // diagnostic builds: 1 = in-place units span-major, last span first
+#endif
+template <bool kTrans, bool kH3 = false, bool kAlign = false, bool kInPlace = false>
 __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     const float* __restrict__ transforms, const float* __restrict__ wfrag16,
     const float* __restrict__ vposed, const float* __restrict__ trans, float* __restrict__ verts,
     int64_t n, int n_verts, int n_groups, const uint16_t* __restrict__ basis_h3, float t_unscale,
     int* __restrict__ status, const float* __restrict__ wfrag16v, int lp, unsigned shifts) {
   static_assert(!(kAlign && kH3), "aligned units: fp32 only");
+  static_assert(!(kInPlace && (kAlign || kH3)), "in-place units: fp32 plain units only");
   __shared__ f32x4 w_lds[kPairMaxGroups * 64];
   __shared__ PairShared sh;
   const int P = kAlign ? 1 << lp : 1;
@@ -658,6 +681,21 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     }
   };
   const int tail_v0 = min(kQVerts * n_full, n_verts - 16);
+  // Unit (q, s) of the worker sequence -> the unit it stands for: itself, or
+  // with the span-major in-place order unit u = q spans + s is span
+  // spans - 1 - u / n_quads of quad u % n_quads (a bijection on the units).
+  constexpr bool kSpanMajor = kInPlace && MANO_PAIR_INPLACE_ORDER == 1;
+  auto unit_of = [&](int64_t uq, int us, int64_t& q2, int& s2) {
+    if constexpr (kSpanMajor) {
+      const uint64_t u = uint64_t(uq) * uint64_t(spans) + uint64_t(us);
+      const uint64_t k = u / uint64_t(n_quads);
+      s2 = spans - 1 - int(k);
+      q2 = int64_t(u - k * uint64_t(n_quads));
+    } else {
+      q2 = uq;
+      s2 = us;
+    }
+  };
   int* full_flag = &sh.full[pair];
   int64_t qd = worker / spans;
   int s = int(worker - qd * spans);
@@ -695,6 +733,23 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       fso[i] = slot0 + unsigned(offsetof(PairStage, rows)) + 4u * unsigned(fr * kPStride + fc);
       tso[i] = slot0 + unsigned(offsetof(PairStage, rows)) + 4u * unsigned(tr * kPStride + tc);
     }
+    // kInPlace: the tail unit's store offsets (floats before ov dropped) and
+    // the straddling float4's b32 / b64 pieces (sweep-0 lanes only)
+    constexpr int kDrop = 0x40000000;  // past any num_records here: the store is dropped
+    const int ov = kInPlace ? 3 * (kQVerts * n_full - tail_v0) : 0;
+    int tvo_ip[kQF4];
+    int p32o = kDrop, p64o = kDrop;
+#pragma unroll
+    for (int i = 0; i < kQF4; ++i) {
+      const int idx = 64 * i + lane;
+      const int it = min(idx, kQHands * tail_rf4 - 1);
+      const int tc = 4 * (it % tail_rf4);
+      tvo_ip[i] = tc >= ov ? tvo[i] : kDrop;
+      if (kInPlace && i == 0 && idx == it && tc < ov && ov < tc + 4) {
+        p32o = (ov & 3) == 2 ? kDrop : tvo[0] + 4 * ((ov & 3) == 1 ? 1 : 3);
+        p64o = (ov & 3) <= 2 ? tvo[0] + 8 : kDrop;
+      }
+    }
     int rvo[kPairRowDmas];  // DMA j: the lane's byte offset in the unit's rows
     int evo[kPairRowDmas];  // kAlign, edge unit: head piece (lanes 0-11), tail piece (12-23)
 #pragma unroll
@@ -712,8 +767,9 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     }
     const int xo = 4 * ((lane / 3) * P * 3 + lane % 3);
     // first hand and hands in the batch of hand quad fq (rows P apart)
+    constexpr bool kReverse = kPairReverse || (kInPlace && !MANO_PAIR_INPLACE_FORWARD && !kSpanMajor);
     auto unit_hands = [&](int64_t fq, int64_t& h0, int& valid) {
-      const int64_t qq = kPairReverse ? n_quads - 1 - fq : fq;
+      const int64_t qq = kReverse ? n_quads - 1 - fq : fq;
       h0 = kAlign ? bcls + int64_t(P) * kQHands * qq : qq * kQHands;
       const int64_t left = kAlign ? (n - 1 - h0) / P + 1 : n - h0;
       valid = int(left < kQHands ? left : kQHands);
@@ -730,9 +786,11 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     // (diagnostic MANO_QUAD_ABLATE & 4: no transform DMA -- stale operands, timing only)
     constexpr int kTrOps = (MANO_QUAD_ABLATE & 4) ? 0 : kQTrF4;
     constexpr int kDmaOps = kPairRowDmas + kTrOps + (kTrans ? 1 : 0);
-    auto dma = [&](int64_t fq, int fs, int slot) {
-      int64_t h0;
-      int valid;
+    constexpr int kStoreOps = 3 + (kInPlace ? 2 : 0);  // per store call, on every path
+    auto dma = [&](int64_t fq0, int fs0, int slot) {
+      int64_t fq, h0;
+      int fs, valid;
+      unit_of(fq0, fs0, fq, fs);
       unit_hands(fq, h0, valid);
       // rows / hands past the batch end are outside num_records (loads give 0)
       const auto rv = rsrc(vposed + h0 * vstride, kAlign ? int64_t(valid - 1) * rstride + vstride : int64_t(valid) * vstride);
@@ -765,10 +823,11 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       return *reinterpret_cast<const __attribute__((address_space(3))) f32x4*>(uintptr_t(addr));
     };
     constexpr unsigned kSlotBytes = sizeof(PairStage);
-    auto store = [&](int64_t fq, int fs, unsigned slot, bool real) {
+    auto store = [&](int64_t fq0, int fs0, unsigned slot, bool real) {
       const unsigned so = slot * kSlotBytes;
-      int64_t h0;
-      int valid;
+      int64_t fq, h0;
+      int fs, valid;
+      unit_of(fq0, fs0, fq, fs);
       unit_hands(fq, h0, valid);
       // not real: num_records 0, every store dropped
       const auto ro = rsrc(verts + h0 * vstride, !real ? 0 : kAlign ? int64_t(valid - 1) * rstride + vstride
@@ -780,8 +839,17 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       for (int i = 0; i < kQF4; ++i) sdata[i] = ds_read4((full ? fso[i] : tso[i]) + so);
 #pragma unroll
       for (int i = 0; i < kQF4; ++i)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sdata[i]), ro, full ? fvo[i] : tvo[i], soff,
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sdata[i]), ro,
+                                               full ? fvo[i] : (kInPlace ? tvo_ip[i] : tvo[i]), soff,
                                                kPairStoreAux);
+      if constexpr (kInPlace) {
+        // scalars first (a bit cast of a vector element reads element 0)
+        const float e1 = sdata[0][1], e2 = sdata[0][2], e3 = sdata[0][3];
+        const float e = (ov & 3) == 1 ? e1 : e3;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(e), ro, full ? kDrop : p32o, soff, kPairStoreAux);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(e2), __float_as_uint(e3)}, ro,
+                                              full ? kDrop : p64o, soff, kPairStoreAux);
+      }
     };
     // Units k + 1 .. k + kAhead - 1 are in flight while unit k is skinned;
     // unit k + kAhead goes into unit k - 2's slot once that is stored.
@@ -792,9 +860,9 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     bool ok = true;
     int64_t qa = qd;  // unit k + kAhead (past the end: the current unit again)
     int sa = s;
-    // Prologue: DMA units 0 .. kAhead - 1 with 3 (dropped) stores after
-    // each, so at every step's wait the ops issued after unit k's DMA are
-    // the same: kAhead - 1 times (3 stores + a DMA).
+    // Prologue: DMA units 0 .. kAhead - 1 with kStoreOps (dropped) stores
+    // after each, so at every step's wait the ops issued after unit k's DMA
+    // are the same: kAhead - 1 times (kStoreOps stores + a DMA).
     // (straight-line: no branch between the prologue's DMA groups, so every
     // control-flow path into the step's wait has the same op sequence --
     // tools/isa_scan.py checks it on the disassembly)
@@ -813,8 +881,9 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     const int64_t n_units = (n_quads * spans - worker + n_workers - 1) / n_workers;  // >= 2
     for (int64_t i = 0; i < n_units; ++i) {
       // unit k = (qd, s) in slot k % kPairSlots: its DMA has landed once at
-      // most (kAhead - 1) (3 + kDmaOps) younger VMEM ops are outstanding.
-      PAIR_TIMED_STMT(asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kAhead - 1) * (3 + kDmaOps)) : "memory"), t_stage);
+      // most (kAhead - 1) (kStoreOps + kDmaOps) younger VMEM ops are outstanding.
+      PAIR_TIMED_STMT(asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kAhead - 1) * (kStoreOps + kDmaOps)) : "memory"),
+                      t_stage);
       pair_signal(full_flag, k + 1);
 #pragma unroll
       for (int j = kPairCompute; j > 0; --j) pend_q[j] = pend_q[j - 1], pend_s[j] = pend_s[j - 1];
@@ -878,6 +947,10 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     }
     ++stamp.units;
     PairStage& st = sh.slot[pair][k % kPairSlots];
+    int64_t q_unit;
+    int s_unit;
+    unit_of(qd, s, q_unit, s_unit);
+    (void)q_unit;
     if (MANO_QUAD_ABLATE & 2) {  // diagnostic: no compute (the memory waves alone)
       pair_signal(&sh.done[pair][k % kPairSlots], k + 1);
 #pragma unroll
@@ -909,8 +982,8 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
         }
       }
       const f16x8* wl = reinterpret_cast<const f16x8*>(w_lds);
-      if (s < n_full) {
-        const int G[4] = {4 * s, 4 * s + 1, 4 * s + 2, 4 * s + 3};
+      if (s_unit < n_full) {
+        const int G[4] = {4 * s_unit, 4 * s_unit + 1, 4 * s_unit + 2, 4 * s_unit + 3};
         const int lv[4] = {0, 16, 32, 48};
         skin_unit4_h3<kTrans, 4, PairStage>(st, wl, ah, tr3, G, lv, hh, cc, v, lane, t_unscale);
       } else {
@@ -929,8 +1002,8 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       for (int t = 0; t < 3; ++t)
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) a[t][kk] = st.tr[a_off[t] + 4 * 12 * kk];
-      if (s < n_full) {
-        const int G[4] = {4 * s, 4 * s + 1, 4 * s + 2, 4 * s + 3};
+      if (s_unit < n_full) {
+        const int G[4] = {4 * s_unit, 4 * s_unit + 1, 4 * s_unit + 2, 4 * s_unit + 3};
         const int lv[4] = {0, 16, 32, 48};
         skin_unit4<kTrans, 4, PairStage>(st, w_lds, a, tr3, G, lv, hh, cc, v, lane);
       } else if constexpr (kAlign) {
@@ -983,6 +1056,21 @@ bool pair_align_ok(const DeviceModel& m) {
   return true;
 }
 
+// The in-place form's launch: skin_pair's fp32 plain units (a batch large
+// enough for one block of them).
+bool skin_in_place_supported(const DeviceModel& m, int64_t n) {
+#if MANO_QUAD_PAIR
+  if (!skin_quad_supported(m) || n <= 0) return false;
+  const int spans = m.n_verts / kQVerts + (m.n_verts % kQVerts ? 1 : 0);
+  const int64_t units = (n + kQHands - 1) / kQHands * spans;
+  return units / (2 * kPairs) >= 1;
+#else
+  (void)m;
+  (void)n;
+  return false;
+#endif
+}
+
 bool skin_quad_supported(const DeviceModel& m) {
 #if MANO_QUAD_PAIR
   if (m.n_groups16 > kPairMaxGroups) return false;
@@ -997,8 +1085,25 @@ bool skin_quad_supported(const DeviceModel& m) {
 // (fp32) or returns hipErrorNotSupported (f16x3: the caller's skin_span_h3).
 hipError_t launch_skin_quad(const DeviceModel& m, int64_t n, const float* transforms,
                             const float* vposed, const float* trans, float* verts,
-                            hipStream_t stream, bool h3) {
+                            hipStream_t stream, bool h3, bool in_place) {
   if (n <= 0) return hipSuccess;
+  if (in_place) {
+#if MANO_QUAD_PAIR
+    if (h3 || !skin_in_place_supported(m, n)) return hipErrorNotSupported;
+    const int64_t units = (n + kQHands - 1) / kQHands * (m.n_verts / kQVerts + (m.n_verts % kQVerts ? 1 : 0));
+    const int64_t blocks_ip = std::min<int64_t>(units / (2 * kPairs), m.n_cu > 0 ? m.n_cu : 1);
+    auto launch_ip = [&](auto kernel) {
+      hipLaunchKernelGGL(kernel, dim3(unsigned(blocks_ip)), dim3(64 * kPairWaves), 0, stream, transforms,
+                         m.wfrag16, vposed, trans, verts, n, m.n_verts, m.n_groups16, m.basis_h3,
+                         m.h3_lbs_unscale, m.status, nullptr, 0, 0u);
+    };
+    if (trans) launch_ip(skin_pair_kernel<true, false, false, true>);
+    else launch_ip(skin_pair_kernel<false, false, false, true>);
+    return hipGetLastError();
+#else
+    return hipErrorNotSupported;
+#endif
+  }
   const int spans = m.n_verts / kQVerts + (m.n_verts % kQVerts ? 1 : 0);
   const int64_t units = (n + kQHands - 1) / kQHands * spans;
   int64_t blocks = (units + kQWaves - 1) / kQWaves;

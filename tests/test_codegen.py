@@ -32,6 +32,18 @@ def report():
     return rep
 
 
+def test_no_slp_vectorize_flag_on_every_build():
+    """The f16x3 kernels' correctness rests on -fno-slp-vectorize (no packed
+    fp32 beside their MFMAs; mano_kernels_h3.hip header): both build recipes
+    -- __graft_entry__.build() and the Makefile -- pass it to every source."""
+    import re
+    import __graft_entry__ as g
+    assert "-fno-slp-vectorize" in g.FLAGS
+    mk = open(os.path.join(REPO, "mano-hand_amd", "Makefile")).read()
+    flags = re.search(r"^CXXFLAGS \?= (.*)$", mk, re.M).group(1).split()
+    assert "-fno-slp-vectorize" in flags
+
+
 def test_kernels_present(report):
     assert report["mfma"].get("v_mfma_f32_16x16x4_f32", 0) > 0       # fp32 kernels
     assert report["mfma"].get("v_mfma_f32_16x16x32_f16", 0) > 0      # f16x3 kernels
@@ -49,9 +61,9 @@ def test_skin_pair_vmcnt_protocol(report):
     """skin_pair's memory wave waits with a hand-counted s_waitcnt vmcnt(N):
     on every control-flow path into that wait the disassembly must end with
     the awaited unit's DMA group, >= 3 stores, then exactly one DMA group
-    (tools/isa_scan.py), in all six instantiations."""
+    (tools/isa_scan.py), in all eight instantiations."""
     pairs = report["skin_pair_vmcnt"]
-    assert len(pairs) == 6, sorted(pairs)  # fp32 x trans x aligned units + f16x3 x trans
+    assert len(pairs) == 8, sorted(pairs)  # fp32 x trans x (plain, aligned, in-place) units + f16x3 x trans
     for name, r in pairs.items():
         assert r["waits"] >= 1 and r["ok"], (name, r)
 

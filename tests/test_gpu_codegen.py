@@ -58,7 +58,7 @@ def test_no_packed_fp32_in_loaded_library():
 def test_skin_pair_vmcnt_protocol_in_loaded_library():
     assert _REPORT is not None, _ERR
     pairs = _REPORT["skin_pair_vmcnt"]
-    assert len(pairs) == 6  # fp32 x trans x aligned units + f16x3 x trans
+    assert len(pairs) == 8  # fp32 x trans x (plain, aligned, in-place) units + f16x3 x trans
     for name, r in pairs.items():
         assert r["ok"], (name, r)
 

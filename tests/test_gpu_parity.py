@@ -455,6 +455,58 @@ def test_standalone_lbs_ragged(engine, dev, params, B, with_trans):
     assert torch.isnan(out[B]).all()
 
 
+@pytest.mark.parametrize("B,with_trans", [(1, True), (2, False), (3, True), (5, False), (1023, True),
+                                         (65537, True), (65538, False)])
+def test_standalone_lbs_in_place(engine, dev, params, B, with_trans):
+    """The LBS in place (mano_stage_skin with rest_verts == verts, ABI 7: the
+    blend GEMM writes v_posed into verts, skin_pair's in-place units
+    overwrite it -- the tail unit stores only its own 10 vertices, hand
+    quads last-first) == the fused kernel's verts bit for bit, ragged
+    batches included; the rows past the batch stay untouched."""
+    rng = np.random.default_rng(700 + B)
+    betas = f32(rng.normal(0, 1, (B, 10)), dev)
+    pose = f32(rng.normal(0, 0.6, (B, 16, 3)), dev)
+    trans = f32(rng.uniform(-1, 1, (B, 3)), dev) if with_trans else None
+    fused = engine.forward(betas, pose, trans)
+    engine.stage_articulate(betas, pose, trans)
+    buf = torch.full((B + 1, 778, 3), float("nan"), device=dev)
+    engine.stage_blend(B, rest_verts=buf[:B])
+    engine.stage_skin(B, buf[:B], rest_verts=buf[:B], trans=trans)
+    torch.cuda.synchronize()
+    assert torch.equal(fused["verts"], buf[:B])
+    assert torch.isnan(buf[B]).all()
+    ref = mano_oracle.forward(params, host(betas[:64]), host(pose[:64]), None if trans is None else host(trans[:64]))
+    assert np.abs(host(buf[:min(B, 64)]) - ref["verts"]).max() <= TOL_M
+
+
+def test_standalone_lbs_in_place_f16x3_and_overlap(engine, dev, params):
+    """In place under F16X3 (no in-place f16x3 kernel: the rows are staged in
+    the workspace first) equals the out-of-place f16x3 LBS bit for bit; rows
+    that overlap without being the same are refused with MANO_EINVAL."""
+    from mano_amd import _abi
+    B = 4099
+    rng = np.random.default_rng(77)
+    betas = f32(rng.normal(0, 1, (B, 10)), dev)
+    pose = f32(rng.normal(0, 0.6, (B, 16, 3)), dev)
+    engine.stage_articulate(betas, pose)
+    vp = torch.empty((B, 778, 3), device=dev)
+    engine.stage_blend(B, rest_verts=vp)
+    engine.set_precision("f16x3")
+    try:
+        out = torch.empty_like(vp)
+        engine.stage_skin(B, out, rest_verts=vp)
+        buf = vp.clone()
+        engine.stage_skin(B, buf, rest_verts=buf)
+        torch.cuda.synchronize()
+        assert torch.equal(out, buf)
+    finally:
+        engine.set_precision("fp32")
+    big = torch.empty((B + 1, 778, 3), device=dev)
+    with pytest.raises(_abi.ManoError) as ei:
+        engine.stage_skin(B, big[1:], rest_verts=big[:B])
+    assert ei.value.code == _abi.MANO_EINVAL and "overlap" in str(ei.value)
+
+
 @pytest.mark.parametrize("B,shared,with_trans", [(1, False, True), (17, True, False),
                                                  (200, False, False), (4096, False, True)])
 def test_forward_equals_staged(engine, dev, params, B, shared, with_trans):

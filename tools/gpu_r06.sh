@@ -29,6 +29,12 @@ for s in ${STEPS:-tests bench}; do
     # box's one GPU, every rank-0 leg on (the CPU baseline at the box's
     # 16-core share instead of cpu_share(8) = 128)
     dp8) step bench_dp8 600 python bench.py --gpus 8 --backend gloo --steps 20 --warmup 5 --cpu-procs 16 ;;
+    # round 6: the in-place LBS (parity, then the A/B against the separate form)
+    inplace_tests) step pytest_inplace 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_codegen.py -m gpu -x -v --timeout 180 --timeout-method thread -k "in_place or standalone or fused_equals or codegen or isa" ;;
+    inplace_ab) step inplace_ab 400 python tools/debug/time_inplace.py libmano_hip.so libmano_hip_ipfwd.so --reps 2 ;;
+    # the driver's N = 8 command with the multi-GPU legs (C3 2^24 and C4 2^22
+    # at their BASELINE sizes), 8 gloo ranks sharing this box's GPU
+    dp8legs) step bench_dp8_legs 600 python bench.py --gpus 8 --backend gloo --steps 20 --warmup 5 --cpu-procs 16 ;;
     stats) step stats 500 rocprofv3 --kernel-trace --stats -d $OUT/stats -o bench --output-format csv -- python bench.py --no-cpu ;;
     *) step extra_$s 600 bash -c "$s" ;;
   esac

@@ -8,7 +8,8 @@
 2. skin_pair's hand-counted vmcnt protocol (mano_skin_quad.hip, memory
    wave): the step's `s_waitcnt vmcnt(N)`, N = (kAhead - 1) * (3 + kDmaOps),
    is correct only if the unit awaited is the DMA group issued 3 + kDmaOps
-   vector-memory ops earlier.  On every control-flow path into each such wait
+   vector-memory ops earlier (5 + kDmaOps in the in-place instantiations:
+   the tail's two partial stores).  On every control-flow path into each such wait
    the disassembly must end with: a DMA group (buffer_load ... lds, the awaited
    unit), at least 3 other vector-memory ops (the stores), then exactly
    kDmaOps LDS-DMA ops (the next unit), so at least N younger ops cover the
@@ -42,8 +43,10 @@ LLVM = "/opt/rocm/llvm/bin"
 PACKED_FP32 = re.compile(r"\bv_pk_(fma|mul|add)_f32\b")
 # skin_pair memory wave: VMEM ops per LDS-DMA of a unit = 4 rows + 3
 # transform sweeps (+ 1 translation load with kTrans), kAhead = 2.
-SKIN_PAIR = re.compile(r"skin_pair_kernelILb([01])ELb([01])E")
+SKIN_PAIR = re.compile(r"skin_pair_kernelILb([01])ELb([01])ELb([01])E(?:Lb([01])E)?")
+# stores per step: 3 sweeps (+ the in-place tail's b32 and b64 pieces, kInPlace)
 K_AHEAD, N_STORES, N_ROWS, N_TR = 2, 3, 4, 3
+N_STORES_IN_PLACE = 5
 
 
 def disassemble(lib=LIB):
@@ -109,14 +112,14 @@ def _vmem_kind(mn, ops):
     return None
 
 
-def check_vmcnt_protocol(insts, n_dma, n_wait):
+def check_vmcnt_protocol(insts, n_dma, n_wait, n_stores=N_STORES):
     """Every path from the function entry to each `s_waitcnt vmcnt(n_wait)`
-    must end with [dma]+ [other]{>=3} [dma]{n_dma} (see the module docstring).
-    Returns (n_waits_found, [failure strings])."""
+    must end with [dma]+ [other]{>=n_stores} [dma]{n_dma} (see the module
+    docstring).  Returns (n_waits_found, [failure strings])."""
     idx = {a: i for i, (a, _, _, _) in enumerate(insts)}
     waits = {i for i, (_, mn, ops, _) in enumerate(insts)
              if mn == "s_waitcnt" and re.search(rf"\bvmcnt\({n_wait}\)", ops)}
-    keep = n_dma + 3 + 8
+    keep = n_dma + n_stores + 8
     failures, seen, stack = [], set(), [(0, ())]
     while stack:
         i, tail = stack.pop()
@@ -136,7 +139,7 @@ def check_vmcnt_protocol(insts, n_dma, n_wait):
                     j -= 1
                 ok = (len(last) == n_dma and all(x == "dma" for x in last)
                       and (k - n_dma - 1 < 0 or tail[k - n_dma - 1] != "dma")
-                      and n_other >= N_STORES and j - 1 >= 0 and tail[j - 1] == "dma")
+                      and n_other >= n_stores and j - 1 >= 0 and tail[j - 1] == "dma")
                 if not ok:
                     failures.append(f"wait at 0x{a:x}: ops before it {list(tail)}")
             kind = _vmem_kind(mn, ops)
@@ -248,11 +251,13 @@ def scan(lib=LIB):
         if not m:
             continue
         trans = m.group(1) == "1"
+        in_place = m.group(4) == "1"
         n_dma = N_ROWS + N_TR + (1 if trans else 0)
-        n_wait = (K_AHEAD - 1) * (N_STORES + n_dma)
-        n_found, fails = check_vmcnt_protocol(insts, n_dma, n_wait)
-        pairs[name] = {"trans": trans, "h3": m.group(2) == "1", "dma_ops": n_dma, "vmcnt": n_wait,
-                       "waits": n_found, "failures": fails[:5], "ok": n_found > 0 and not fails}
+        n_st = N_STORES_IN_PLACE if in_place else N_STORES
+        n_wait = (K_AHEAD - 1) * (n_st + n_dma)
+        n_found, fails = check_vmcnt_protocol(insts, n_dma, n_wait, n_st)
+        pairs[name] = {"trans": trans, "h3": m.group(2) == "1", "in_place": in_place, "dma_ops": n_dma,
+                       "vmcnt": n_wait, "waits": n_found, "failures": fails[:5], "ok": n_found > 0 and not fails}
     packed = [l.strip() for l in asm.splitlines() if PACKED_FP32.search(l)]
     return asm, {"packed_fp32": len(packed), "packed_fp32_examples": packed[:5],
                  "skin_pair_vmcnt": pairs,
