@@ -147,9 +147,11 @@ def parse(argv=None):
     ap.add_argument("--event-every", type=int, default=8,
                     help="bracket the kernels of every E-th timed step with HIP events (1 = every step; "
                          "each timing event costs the step ~4 us, tools/debug/time_events.py)")
-    ap.add_argument("--path", choices=("forward", "api", "unfused"), default="forward",
+    ap.add_argument("--path", choices=("forward", "api", "unfused", "unfused_separate"), default="forward",
                     help="forward: mano_forward's two kernels, each bracketed by events (default); "
-                         "api: one mano_forward call per step; unfused: articulate + blend + skin")
+                         "api: one mano_forward call per step; unfused: articulate + blend (v_posed into "
+                         "verts) + the LBS in place over verts (ABI 7); unfused_separate: the same with "
+                         "v_posed in the workspace and the LBS out of place")
     ap.add_argument("--precision", choices=("fp32", "f16x3"), default="fp32",
                     help="fp32: exact fp32 MFMA (default); f16x3: split-half MFMA "
                          "(include/mano_hip.h MANO_PRECISION_F16X3)")
@@ -736,7 +738,8 @@ def load_traffic(path, kernel, batch):
 
 # Demangled-name fragment of each dominant kernel (rocprofv3 Kernel_Name).
 PMC_KERNEL_NAME = {"blend_skin": "::blend_skin16_kernel<", "blend_skin_h3": "::blend_skin_h3_kernel<",
-                   "blend": "::blend_kernel(", "skin": "::skin_pair_kernel<", "mano_forward": "::blend_skin16_kernel<"}
+                   "blend": "::blend_kernel(", "skin": "::skin_pair_kernel<", "mano_forward": "::blend_skin16_kernel<",
+                   "blend_separate": "::blend_kernel(", "skin_separate": "::skin_pair_kernel<"}
 
 
 def pmc_values(d, counter, name_fragment):
@@ -1130,7 +1133,17 @@ def run(args, wd):
         elif path == "api":
             model.forward(betas, pose, trans, joints=True, out={"verts": vo, "joints": jo})
             mark(1)
-        else:  # unfused: articulate, blend GEMM (v_posed to HBM), LBS
+        elif path == "unfused" and model.precision == "fp32":
+            # articulate, blend GEMM (v_posed into verts), the LBS in place (f16x3
+            # has no in-place kernel: it would stage the rows first, so it takes
+            # the separate form below)
+            model.stage_articulate(betas, pose, trans, joints=jo)
+            mark(1)
+            model.stage_blend(B, rest_verts=vo)
+            mark(2)
+            model.stage_skin(B, vo, rest_verts=vo, trans=trans)
+            mark(3)
+        else:  # unfused_separate (and f16x3's unfused): v_posed in the workspace, the LBS into verts
             model.stage_articulate(betas, pose, trans, joints=jo)
             mark(1)
             model.stage_blend(B)
@@ -1138,7 +1151,7 @@ def run(args, wd):
             model.stage_skin(B, vo, trans=trans)
             mark(3)
 
-    n_marks = {"forward": 3, "api": 2, "unfused": 4}
+    n_marks = {"forward": 3, "api": 2, "unfused": 4, "unfused_separate": 4}
 
     def step(marks=None, gmarks=None):
         run_path(args.path, marks)
@@ -1232,7 +1245,8 @@ def run(args, wd):
     # not part of `value`), so every kernel's roofline is reported each run.
     timed = {"forward": {"articulate": (0, 1), "blend_skin": (1, 2)},
              "api": {"mano_forward": (0, 1)},
-             "unfused": {"articulate": (0, 1), "blend": (1, 2), "skin": (2, 3)}}
+             "unfused": {"articulate": (0, 1), "blend": (1, 2), "skin": (2, 3)},
+             "unfused_separate": {"blend_separate": (1, 2), "skin_separate": (2, 3)}}
     sampled = [e for e in events if e is not None]
     ms = {k: span(a, b, sampled) for k, (a, b) in timed[args.path].items()}
     other = {"fp32": "f16x3", "f16x3": "fp32"}[args.precision]
@@ -1251,7 +1265,7 @@ def run(args, wd):
             torch.cuda.synchronize()
             for k, (a, b) in timed[path].items():
                 into.setdefault(k, span(a, b, evs))
-        for path in ("forward", "api", "unfused"):
+        for path in ("forward", "api", "unfused", "unfused_separate"):
             if path != args.path:
                 time_path(path, ms)
         # The standalone LBS back to back (each launch after another LBS
@@ -1317,7 +1331,8 @@ def run(args, wd):
         return nbytes * B / (t * 1e-3) / 1e9
 
     in_path = {"forward": ("articulate", "blend_skin"), "api": ("mano_forward",),
-               "unfused": ("articulate", "blend", "skin")}[args.path]
+               "unfused": ("articulate", "blend", "skin"),
+               "unfused_separate": ("articulate", "blend_separate", "skin_separate")}[args.path]
     kernels = {}
     if "mano_forward" in ms:
         kernels["mano_forward"] = {"kernel": "articulate_kernel + blend_skin16_kernel (one ABI call)",
@@ -1364,6 +1379,20 @@ def run(args, wd):
             kernels["skin"].update({"ms_back_to_back": b2b, "achieved_GBs_back_to_back": gbs(SKIN_BYTES_PER_HAND, b2b),
                                     "frac_back_to_back": gbs(SKIN_BYTES_PER_HAND, b2b) / PEAK_HBM_GBS,
                                     "timing_back_to_back": "one HIP event pair around 50 launches after 50 warm ones"})
+    if "skin" in kernels:
+        kernels["skin"]["form"] = ("in place over verts (mano_stage_skin rest_verts == verts, ABI 7), after the "
+                                   "blend GEMM wrote v_posed into verts" if args.precision == "fp32" else
+                                   "out of place (f16x3 has no in-place kernel)")
+    if "blend_separate" in ms:
+        a = tflops(BLEND_FLOP_PER_HAND, ms["blend_separate"])
+        kernels["blend_separate"] = {"kernel": "blend_kernel (v_posed into the workspace)",
+                                     "ms": ms["blend_separate"], "bound": "mfma", "achieved_TFLOPs": a,
+                                     "frac": a / PEAK_FP32_TFLOPS, "flop_per_hand": BLEND_FLOP_PER_HAND}
+    if "skin_separate" in ms:
+        a = gbs(SKIN_BYTES_PER_HAND, ms["skin_separate"])
+        kernels["skin_separate"] = {"kernel": "skin_pair_kernel (out of place, workspace v_posed -> verts)",
+                                    "ms": ms["skin_separate"], "bound": "hbm", "achieved_GBs": a,
+                                    "frac": a / PEAK_HBM_GBS, "bytes_per_hand": SKIN_BYTES_PER_HAND}
     for k, v in kernels.items():
         v["in_timed_path"] = k in in_path
         v["precision"] = args.precision
@@ -1388,6 +1417,8 @@ def run(args, wd):
     # Roofline of the dominant kernel of the timed path.
     if args.path == "unfused":
         dominant = "blend" if ms["blend"] >= ms["skin"] else "skin"
+    elif args.path == "unfused_separate":
+        dominant = "blend_separate" if ms["blend_separate"] >= ms["skin_separate"] else "skin_separate"
     elif args.path == "api":
         dominant = "blend_skin" if "blend_skin" in kernels else None
     else:
