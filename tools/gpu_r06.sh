@@ -37,6 +37,9 @@ for s in ${STEPS:-tests bench}; do
     # the driver's N = 8 command with the multi-GPU legs (C3 2^24 and C4 2^22
     # at their BASELINE sizes), 8 gloo ranks sharing this box's GPU
     dp8legs) step bench_dp8_legs 600 python bench.py --gpus 8 --backend gloo --steps 20 --warmup 5 --cpu-procs 16 ;;
+    # the RCCL form of the multi-GPU legs at BASELINE sizes, one rank (C3: the
+    # whole 2^24 batch on this GPU; C4: 2^22 + mano_gather + the ring copy)
+    legs1) step bench_legs1 600 python bench.py --force-pg --backend nccl --legs on --steps 20 --warmup 5 --no-cpu --no-dropin ;;
     stats) step stats 500 rocprofv3 --kernel-trace --stats -d $OUT/stats -o bench --output-format csv -- python bench.py --no-cpu ;;
     *) step extra_$s 600 bash -c "$s" ;;
   esac
