@@ -608,14 +608,15 @@ def run_legs(args, plan, model, rank, world, dev, local_dev, wd, skipped):
 
         host_gather = gather and not nccl
         steps = 1 if host_gather else max(1, args.leg_steps)
+        stream = torch.cuda.current_stream(dev)
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+        gather_host_s = []
         if not host_gather:       # one untimed step (C4 on RCCL: RCCL sets up its channels)
             fwd()
             if gather:
                 gath()
-        torch.cuda.synchronize()
-        stream = torch.cuda.current_stream(dev)
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
-        gather_host_s = []
+        # no sync before the barrier: the GPU works through the rendezvous (the
+        # untimed step warms the clock; an idle gap would cool it again)
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -1162,35 +1163,45 @@ def run(args, wd):
             if gmarks is not None:
                 gmarks[1].record(stream)
 
-    # Clock ramp, then the untimed warmup.  With a process group the ranks
-    # agree on when the ramp ends (one small all_reduce per 10 steps): with
-    # the C4 gather every step is a collective, and ranks that each read
-    # their own clock could run different numbers of ramp steps -- the
-    # unmatched gathers would hang.
+    # Clock ramp, then the untimed warmup, with no idle GPU before the timed
+    # region: the chip needs ~50 back-to-back launches to reach its steady
+    # clock and loses it in a ~millisecond idle gap (blend_skin16 545-555 vs
+    # 485 us, §4 round 4; round 6: a process-group run that paused for a
+    # collective every 10 ramp steps and for the pre-timing barrier timed its
+    # 20 steps at 0.551 ms, `profiles/r06/r06e_legs1_bench.json`).  So the
+    # ramp's length is fixed up front -- 10 steps, then 10 more on the host
+    # clock give the step time -- and, with a process group, agreed once by
+    # the ranks (MAX: with the C4 gather every step is a collective, so every
+    # rank must run the same number); the rest of the ramp, the warmup and
+    # the barrier then follow with no sync: the barrier's collective is
+    # ordered after the warmup on the stream (nccl), or waits on the host
+    # while the GPU works (gloo).
     wd.enter("ramp")
     t_ramp = time.perf_counter()
-    n_ramp = 0
-    while True:
-        for _ in range(10):
-            step()
-        n_ramp += 10
-        torch.cuda.synchronize()
-        done = time.perf_counter() - t_ramp >= args.ramp_seconds
-        if args.inject_hang == rank and dist_on:
-            while True:       # (tests) this rank stalls outside the ramp's collective
-                time.sleep(0.5)
-        if dist_on:
-            flag = torch.tensor([1 if done else 0], device=dev if args.backend == "nccl" else "cpu",
-                                dtype=torch.int32)
-            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
-            done = bool(flag.item())
-        if done:
-            break
-    t_ramp = time.perf_counter() - t_ramp
+    for _ in range(10):
+        step()
+    torch.cuda.synchronize()
+    t_cal = time.perf_counter()
+    for _ in range(10):
+        step()
+    torch.cuda.synchronize()
+    per_step = max(1e-6, (time.perf_counter() - t_cal) / 10)
+    n_more = max(0, int(np.ceil((args.ramp_seconds - (time.perf_counter() - t_ramp)) / per_step)))
+    if args.inject_hang == rank and dist_on:
+        while True:       # (tests) this rank stalls outside the ramp's collective
+            time.sleep(0.5)
+    if dist_on:
+        agreed = torch.tensor([n_more], device=dev if args.backend == "nccl" else "cpu", dtype=torch.int64)
+        dist.all_reduce(agreed, op=dist.ReduceOp.MAX)
+        n_more = int(agreed.item())
+    t_agreed = time.perf_counter() - t_ramp
+    for _ in range(n_more):
+        step()
+    n_ramp = 20 + n_more
+    t_ramp = t_agreed + n_more * per_step    # the ramp's GPU time (its tail is still running here)
     wd.enter("warmup")
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
 
     # Per-kernel durations come from HIP events on the launch stream around
     # the kernels of every E-th timed step (E = --event-every): a timing event
@@ -1206,7 +1217,7 @@ def run(args, wd):
     wd.enter("timed")
     if dist_on:
         dist.barrier()
-    torch.cuda.synchronize()
+    torch.cuda.synchronize()   # the ramp and warmup end here: the GPU has not idled since the ramp began
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(events[i], gevents[i])
@@ -1557,7 +1568,7 @@ def run(args, wd):
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ramp": {"seconds": t_ramp, "steps": n_ramp},
+            "ramp": {"seconds": t_ramp, "steps": n_ramp, "step_ms": per_step * 1e3},
             "kernel_events": {"every": every, "sampled_steps": len(sampled)},
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,

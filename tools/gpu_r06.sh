@@ -40,6 +40,8 @@ for s in ${STEPS:-tests bench}; do
     # the RCCL form of the multi-GPU legs at BASELINE sizes, one rank (C3: the
     # whole 2^24 batch on this GPU; C4: 2^22 + mano_gather + the ring copy)
     legs1) step bench_legs1 600 python bench.py --force-pg --backend nccl --legs on --steps 20 --warmup 5 --no-cpu --no-dropin ;;
+    dist_tests) step pytest_dist 600 python -u -m pytest tests/test_gpu_distributed.py tests/test_gpu_multi_device.py -m gpu -x -v --timeout 180 --timeout-method thread ;;
+    pg1) step bench_pg1 300 python bench.py --force-pg --backend nccl --steps 20 --warmup 5 --no-cpu --no-dropin --legs off ;;
     stats) step stats 500 rocprofv3 --kernel-trace --stats -d $OUT/stats -o bench --output-format csv -- python bench.py --no-cpu ;;
     *) step extra_$s 600 bash -c "$s" ;;
   esac
