@@ -42,6 +42,12 @@ for s in ${STEPS:-tests bench}; do
     legs1) step bench_legs1 600 python bench.py --force-pg --backend nccl --legs on --steps 20 --warmup 5 --no-cpu --no-dropin ;;
     dist_tests) step pytest_dist 600 python -u -m pytest tests/test_gpu_distributed.py tests/test_gpu_multi_device.py -m gpu -x -v --timeout 180 --timeout-method thread ;;
     pg1) step bench_pg1 300 python bench.py --force-pg --backend nccl --steps 20 --warmup 5 --no-cpu --no-dropin --legs off ;;
+    # kernel traces of the timed steps: N = 1, and one rank under a process group (nccl, gloo)
+    trace_pg) B="python bench.py --steps 20 --warmup 5 --no-extra --no-check --no-dropin --no-cpu --no-live-pmc"
+       step trace_n1 300 rocprofv3 --kernel-trace -d $OUT/tr_n1 -o t --output-format csv -- $B
+       WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29611 step trace_nccl 300 rocprofv3 --kernel-trace -d $OUT/tr_nccl -o t --output-format csv -- $B --force-pg --backend nccl --legs off
+       WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29612 step trace_gloo 300 rocprofv3 --kernel-trace -d $OUT/tr_gloo -o t --output-format csv -- $B --force-pg --backend gloo --legs off
+       for t in n1 nccl gloo; do echo "$t $(python tools/trace_steps.py $OUT/tr_$t)"; done | tee $OUT/trace_steps.txt ;;
     stats) step stats 500 rocprofv3 --kernel-trace --stats -d $OUT/stats -o bench --output-format csv -- python bench.py --no-cpu ;;
     *) step extra_$s 600 bash -c "$s" ;;
   esac
