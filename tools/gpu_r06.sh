@@ -48,6 +48,14 @@ for s in ${STEPS:-tests bench}; do
        WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29611 step trace_nccl 300 rocprofv3 --kernel-trace -d $OUT/tr_nccl -o t --output-format csv -- $B --force-pg --backend nccl --legs off
        WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29612 step trace_gloo 300 rocprofv3 --kernel-trace -d $OUT/tr_gloo -o t --output-format csv -- $B --force-pg --backend gloo --legs off
        for t in n1 nccl gloo; do echo "$t $(python tools/trace_steps.py $OUT/tr_$t)"; done | tee $OUT/trace_steps.txt ;;
+    # the process group's cost on one GPU: plain, gloo group, nccl group alternating
+    pg_ab) F="--steps 20 --warmup 5 --no-extra --no-check --no-dropin --no-cpu --no-live-pmc --legs off"
+       for i in 1 2 3; do
+         step ab_plain_$i 120 python bench.py $F
+         step ab_gloo_$i 120 python bench.py $F --force-pg --backend gloo
+         step ab_nccl_$i 120 python bench.py $F --force-pg --backend nccl
+       done
+       for f in $OUT/ab_*.log; do echo "$(basename $f) $(grep '^{' $f | tail -1 | python -c 'import json,sys; l=json.load(sys.stdin); k=l["kernels"]; print(round(l["ms_per_step"],4), round(k["articulate"]["ms"],4), round(k["blend_skin"]["ms"],4))')"; done | tee $OUT/pg_ab.txt ;;
     stats) step stats 500 rocprofv3 --kernel-trace --stats -d $OUT/stats -o bench --output-format csv -- python bench.py --no-cpu ;;
     *) step extra_$s 600 bash -c "$s" ;;
   esac
