@@ -1215,13 +1215,20 @@ def run(args, wd):
     gevents = [[torch.cuda.Event(enable_timing=True) for _ in range(2)]
                if gather_on and i % every == 0 else None for i in range(args.steps)]
     wd.enter("timed")
+    t_open = time.perf_counter()
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize()   # the ramp and warmup end here: the GPU has not idled since the ramp began
     t0 = time.perf_counter()
+    span0 = torch.cuda.Event(enable_timing=True)
+    span1 = torch.cuda.Event(enable_timing=True)
+    span0.record(stream)
     for i in range(args.steps):
         step(events[i], gevents[i])
+    span1.record(stream)
+    t_issued = time.perf_counter()
     torch.cuda.synchronize()
+    t_synced = time.perf_counter()
     if dist_on:
         # Every rank's GPU work is done (the sync above): the closing barrier
         # only has to meet the ranks, so it runs on the host-side gloo group
@@ -1232,6 +1239,12 @@ def run(args, wd):
         # stream, so the ranks start together once every GPU is ready.
         dist.barrier(group=end_group)
     dt = time.perf_counter() - t0
+    # where the timed region's host time went (this rank): issuing the K
+    # steps, waiting for the GPU to finish them, the closing barrier; and the
+    # opening barrier + sync before t0 (outside the region)
+    region = {"issue_s": t_issued - t0, "sync_s": t_synced - t_issued, "closing_barrier_s": t0 + dt - t_synced,
+              "opening_barrier_and_sync_s": t0 - t_open,
+              "gpu_ms_per_step": span0.elapsed_time(span1) / args.steps}
     if dist_on:
         t = torch.tensor([dt], device=dev if args.backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -1577,6 +1590,7 @@ def run(args, wd):
             "warmup": args.warmup,
             "ramp": {"seconds": t_ramp, "steps": n_ramp, "step_ms": per_step * 1e3},
             "kernel_events": {"every": every, "sampled_steps": len(sampled)},
+            "timed_region_rank0": region,
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
