@@ -959,8 +959,9 @@ def run_single_process(args):
         step()
     sync_all()
     every = max(1, min(args.event_every, args.steps // 5))
+    first = 1 % every if args.steps > 1 else 0   # not step 0 (run(): its bracket holds the host's launch latency)
     n_marks = 4 if gather else 3
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(n_marks)] if i % every == 0 else None
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(n_marks)] if i % every == first else None
               for i in range(args.steps)]
     sync_all()
     t0 = time.perf_counter()
@@ -1208,12 +1209,18 @@ def run(args, wd):
     # is a release point on the stream, which costs the step ~4 us per event
     # (0.530 vs 0.518 ms with three per step, tools/debug/time_events.py), so
     # bracketing every step would bill the instrumentation to `value`.
+    # Steps 1, 1 + E, ... are sampled, not step 0: the first timed step's
+    # opening event is reached by an idle GPU right after the sync, before
+    # the host has issued the articulation behind it, so its bracket would
+    # hold the host's launch latency (0.035-0.054 ms by events vs 23.6 us by
+    # rocprof's trace, r06f / r06g).
     every = max(1, min(args.event_every, args.steps // 5))  # at least 5 sampled steps
+    first = 1 % every if args.steps > 1 else 0
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(n_marks[args.path])]
-              if i % every == 0 else None for i in range(args.steps)]
+              if i % every == first else None for i in range(args.steps)]
     # the gather of the same sampled steps, bracketed on the same stream
     gevents = [[torch.cuda.Event(enable_timing=True) for _ in range(2)]
-               if gather_on and i % every == 0 else None for i in range(args.steps)]
+               if gather_on and i % every == first else None for i in range(args.steps)]
     wd.enter("timed")
     t_open = time.perf_counter()
     if dist_on:
