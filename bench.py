@@ -438,6 +438,18 @@ def sample_indices(B, n_random=48, seed=0):
     return np.unique(np.clip(np.concatenate([edges, rnd]), 0, B - 1))
 
 
+def event_plan(steps, event_every):
+    """(E, first): the timed steps whose kernels get HIP events are
+    first, first + E, ... -- at least 5 of them (E = min(--event-every,
+    steps // 5)), and not step 0 when there is a choice: the first timed
+    step's opening event is reached by an idle GPU right after the sync,
+    before the host has issued the kernel behind it, so its bracket would
+    hold the host's launch latency (0.035-0.054 ms by events vs 23.6 us by
+    rocprof's trace for the articulation, r06f / r06g)."""
+    every = max(1, min(event_every, steps // 5))
+    return every, (1 % every if steps > 1 else 0)
+
+
 def check_sample(model, seed, first, B, betas, pose, trans, verts, joints, model_path, with_trans,
                  tol=1e-5):
     """Max |GPU - oracle| over sampled hands of the timed step's outputs: the
@@ -958,8 +970,7 @@ def run_single_process(args):
     for _ in range(args.warmup):
         step()
     sync_all()
-    every = max(1, min(args.event_every, args.steps // 5))
-    first = 1 % every if args.steps > 1 else 0   # not step 0 (run(): its bracket holds the host's launch latency)
+    every, first = event_plan(args.steps, args.event_every)
     n_marks = 4 if gather else 3
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(n_marks)] if i % every == first else None
               for i in range(args.steps)]
@@ -1209,13 +1220,8 @@ def run(args, wd):
     # is a release point on the stream, which costs the step ~4 us per event
     # (0.530 vs 0.518 ms with three per step, tools/debug/time_events.py), so
     # bracketing every step would bill the instrumentation to `value`.
-    # Steps 1, 1 + E, ... are sampled, not step 0: the first timed step's
-    # opening event is reached by an idle GPU right after the sync, before
-    # the host has issued the articulation behind it, so its bracket would
-    # hold the host's launch latency (0.035-0.054 ms by events vs 23.6 us by
-    # rocprof's trace, r06f / r06g).
-    every = max(1, min(args.event_every, args.steps // 5))  # at least 5 sampled steps
-    first = 1 % every if args.steps > 1 else 0
+    # Steps first, first + E, ... (event_plan: at least 5, not step 0).
+    every, first = event_plan(args.steps, args.event_every)
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(n_marks[args.path])]
               if i % every == first else None for i in range(args.steps)]
     # the gather of the same sampled steps, bracketed on the same stream

@@ -253,3 +253,15 @@ def test_pmc_child_measures_the_timed_path_only():
     assert "--no-dropin" in child and "--no-check" in child and "--no-live-pmc" in child
     parsed = bench.parse(child)
     assert parsed.no_dropin and parsed.batch == 65536 and parsed.path == args.path
+
+
+def test_event_plan_skips_step_zero():
+    """The sampled timed steps: at least 5, never step 0 when there is a
+    choice (its bracket holds the host's first launch latency)."""
+    for steps, ev in [(20, 8), (200, 8), (10, 8), (7, 8), (5, 8), (1, 8), (20, 1)]:
+        every, first = bench.event_plan(steps, ev)
+        picked = [i for i in range(steps) if i % every == first]
+        assert len(picked) >= min(5, steps - (1 if every > 1 else 0)) and len(picked) >= 1
+        if every > 1:
+            assert 0 not in picked
+    assert bench.event_plan(20, 8) == (4, 1)                 # the driver's 20 steps: 1, 5, 9, 13, 17
