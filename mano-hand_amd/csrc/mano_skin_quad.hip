@@ -609,7 +609,12 @@ struct PairStamp {
 // outputs it does not store.  Hand quads go last-first: the blend GEMM's last
 // ~256 MB of v_posed are still dirty in the Infinity Cache when the LBS
 // starts, so their reads hit and their lines are overwritten in the cache
-// instead of being written back first.
+// instead of being written back first.  (In place,
+// `vposed` and `verts` alias despite their __restrict__: the kernel touches
+// both only through buffer intrinsics on resource descriptors -- the rows'
+// LDS-DMA and the memory wave's stores, ordered by its counted vmcnt -- never
+// through the pointers themselves, and distinct units' bytes are disjoint
+// apart from the tail reads above.)
 #ifndef MANO_PAIR_INPLACE_FORWARD
 #define MANO_PAIR_INPLACE_FORWARD 0  // diagnostic builds: 1 = in-place units in hand order
 #endif
