@@ -197,6 +197,9 @@ def parse(argv=None):
     ap.add_argument("--inject-hang", type=int, default=None,
                     help="(tests) this rank skips a collective and stalls: the launch check's all_reduce, "
                          "or with a process group the clock ramp's")
+    ap.add_argument("--inject-hang-leg", type=int, default=None,
+                    help="(tests) this rank stalls at the start of leg C4: the watchdog's leg path (the line "
+                         "keeps the headline and names the hung leg, every rank exits 0)")
     ap.add_argument("--single-process", action="store_true",
                     help="ONE process and host thread drive --gpus N devices (mano_amd.ManoMultiDevice; "
                          "the gather is one RCCL group from that thread, ABI 6) instead of N torchrun ranks")
@@ -251,6 +254,12 @@ class Watchdog:
         self.phases = []
         self.deadline = None
         self._thread = None
+        # Set once the headline is measured (rank 0: its finished line; the
+        # other ranks: {}), with `legs` the dict the legs fill: a watchdog
+        # firing inside a leg then prints that line -- the headline intact,
+        # the finished legs, the hung one named -- and every rank exits 0.
+        self.partial = None
+        self.legs = None
 
     def enter(self, phase):
         self.phase = phase
@@ -283,6 +292,23 @@ class Watchdog:
                 self.fire()
 
     def fire(self):
+        if self.partial is not None and self.phase.startswith("leg_"):
+            # a multi-GPU leg hung (not part of `value`): keep the headline
+            if self.rank == 0:
+                line = dict(self.partial)
+                line["legs"] = dict(self.legs or {})
+                line["legs"]["hung"] = {"phase": self.phase, "elapsed_s": round(time.monotonic() - T_START, 3),
+                                        "note": "watchdog inside a leg; the headline above is complete"}
+                line["status"] = "ok"
+                line["run"] = {"wall_s": round(time.monotonic() - T_START, 3), "phases": self.phases,
+                               "skipped_legs": {"rank0_legs": "a multi-GPU leg hung (watchdog)"}}
+                print(json.dumps(line), flush=True)
+            sys.stderr.write(f"bench: rank {self.rank}/{self.world}: watchdog inside {self.phase!r} after "
+                             f"{time.monotonic() - T_START:.1f} s; Python stacks of every thread:\n")
+            sys.stderr.flush()
+            faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+            sys.stderr.flush()
+            os._exit(0)
         line = status_line("watchdog", self.phase, self.rank, self.world, phases=self.phases)
         print(json.dumps(line), file=sys.stdout if self.rank == 0 else sys.stderr, flush=True)
         sys.stderr.write(f"bench: rank {self.rank}/{self.world}: watchdog after {line['elapsed_s']} s "
@@ -542,7 +568,7 @@ def check_gather(model, seed, B, world, gv, gj, with_trans, per_rank=64, ranges=
                       "by global index, forwards them locally, compares with GPU 0's gathered verts / joints"}
 
 
-def run_legs(args, plan, model, rank, world, dev, local_dev, wd, skipped):
+def run_legs(args, plan, model, rank, world, dev, local_dev, wd, skipped, out=None):
     """BASELINE's multi-GPU configs, after the headline (not part of `value`).
 
     C3: the 2^24-hand global batch split over the ranks (rank r: hands
@@ -562,7 +588,8 @@ def run_legs(args, plan, model, rank, world, dev, local_dev, wd, skipped):
     from mano_amd.distributed import AbiGather, gather_rows_to_root, shard_range
     nccl = args.backend == "nccl"
     red_dev = dev if nccl else "cpu"
-    out, gatherer = {}, None
+    out = {} if out is None else out
+    gatherer = None
     last_note = [0.0]
 
     def note(done, total):
@@ -572,15 +599,8 @@ def run_legs(args, plan, model, rank, world, dev, local_dev, wd, skipped):
             last_note[0] = time.monotonic()
             print(f"bench: {wd.phase}: gathered {done} of {total} rows per rank "
                   f"({time.monotonic() - T_START:.0f} s)", file=sys.stderr, flush=True)
-    for name, p in plan.items():
-        # the ranks agree to start a leg (it must end before the watchdog)
-        left = (T_START + args.watchdog_seconds - time.monotonic()) if args.watchdog_seconds > 0 else 1e9
-        go = torch.tensor([1 if left >= args.leg_min_seconds else 0], device=red_dev, dtype=torch.int32)
-        dist.all_reduce(go, op=dist.ReduceOp.MIN)
-        if not int(go.item()):
-            skipped[f"leg_{name}"] = (f"{left:.0f} s left before --watchdog-seconds on rank {rank} "
-                                      f"(a leg needs --leg-min-seconds {args.leg_min_seconds:.0f})")
-            continue
+    def one_leg(name, p):
+        nonlocal gatherer
         wd.enter(f"leg_{name}")
         if rank == 0:
             print(f"bench: leg {name}: {p['global_batch']} hands over {world} ranks "
@@ -718,10 +738,30 @@ def run_legs(args, plan, model, rank, world, dev, local_dev, wd, skipped):
             del av, aj
             dist.barrier()
         res["wall_s"] = round(time.monotonic() - t_leg, 3)
-        out[name] = res
-        del inp, ws, gv, gj, verts, joints
+        return res
+
+    for name, p in plan.items():
+        # the ranks agree to start a leg (it must end before the watchdog)
+        left = (T_START + args.watchdog_seconds - time.monotonic()) if args.watchdog_seconds > 0 else 1e9
+        go = torch.tensor([1 if left >= args.leg_min_seconds else 0], device=red_dev, dtype=torch.int32)
+        dist.all_reduce(go, op=dist.ReduceOp.MIN)
+        if not int(go.item()):
+            skipped[f"leg_{name}"] = (f"{left:.0f} s left before --watchdog-seconds on rank {rank} "
+                                      f"(a leg needs --leg-min-seconds {args.leg_min_seconds:.0f})")
+            continue
+        if args.inject_hang_leg == rank and name == "C4":
+            wd.enter("leg_C4")
+            while True:       # (tests) this rank stalls outside the leg's first collective
+                time.sleep(0.5)
+        try:
+            out[name] = one_leg(name, p)
+        except Exception as e:   # a symmetric failure (e.g. RCCL refused): the headline stands
+            out[name] = {"error": f"{type(e).__name__}: {e}"[:500], "phase": wd.phase,
+                         "wall_s": round(time.monotonic() - T_START, 3)}
+            print(f"bench: rank {rank}: leg {name} failed in {wd.phase}: {type(e).__name__}: {e}",
+                  file=sys.stderr, flush=True)
         torch.cuda.synchronize()
-        torch.cuda.empty_cache()
+        torch.cuda.empty_cache()     # the leg's buffers are gone with one_leg's frame
     if gatherer is not None:
         gatherer.close()
     return out
@@ -1513,10 +1553,62 @@ def run(args, wd):
         if args.dump_gather:
             np.savez(args.dump_gather, verts=gv.cpu().numpy(), joints=gj.cpu().numpy())
 
+    # The headline is measured and checked: rank 0's line, before anything
+    # that could hang (the roofline's traffic and the host legs fill it in
+    # later).
+    line = None
+    if rank == 0:
+        total = B * world * args.steps
+        line = {
+            "metric": METRIC,
+            "value": total / dt,
+            "unit": "hands/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ramp": {"seconds": t_ramp, "steps": n_ramp, "step_ms": per_step * 1e3},
+            "kernel_events": {"every": every, "sampled_steps": len(sampled)},
+            "timed_region_rank0": region,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.precision,
+            "data": "synthetic (random-init MANO arrays of the official shapes, seed 0; "
+                    "Philox inputs keyed by (seed, global hand index): beta ~ N(0,1), "
+                    "pose ~ N(0,0.5^2) rad" + (", trans ~ U(-1,1) m" if with_trans else "") +
+                    ", generated on device)",
+            "config": {"workload": wl["desc"] if B == wl["hands"] else f"{args.workload} at {B} hands per GPU",
+                       "hands_per_gpu": B, "global_batch": B * world,
+                       "outputs": "verts+joints", "trans": with_trans, "path": args.path,
+                       "gather_to_gpu0": gather_on,
+                       "gather_impl": None if not gather_on else
+                       ({"sendrecv": "mano_gather (RCCL send/recv)", "allgather": "mano_allgather (RCCL ring)"}[impl]
+                        if gatherer is not None else "gloo rehearsal"),
+                       "parallelism": f"dp{world}"},
+            "process_group": ({"backend": args.backend, "world": world, "forced_at_one_rank": world == 1}
+                              if dist_on else None),
+            "roofline": roof,
+            "kernels": kernels,
+            "correctness": correctness,
+            "device_status": device_status,
+        }
+        if gather_info is not None:
+            line["gather"] = gather_info
+        if gather_check is not None:
+            line["gather_check"] = gather_check
+
     # BASELINE's multi-GPU configs (C3, C4) as legs after the headline: every
-    # N > 1 run measures them (not part of `value`), inside the watchdog.
+    # N > 1 run measures them (not part of `value`), inside the watchdog --
+    # which, if a leg hangs, prints the line above with the finished legs
+    # instead of a bare status line (Watchdog.partial).
     legs_plan = plan_legs(args, world) if dist_on else {}
-    legs = run_legs(args, legs_plan, model, rank, world, dev, local_dev, wd, skipped) if legs_plan else None
+    legs = None
+    if legs_plan:
+        legs = {}
+        wd.partial, wd.legs = (line if rank == 0 else {}), legs
+        run_legs(args, legs_plan, model, rank, world, dev, local_dev, wd, skipped, out=legs)
+        wd.partial = None
 
     # The collective phases are over.  Rank 0's host legs hold no collective
     # and each is bounded by its own child timeout, fitted into the deadline;
@@ -1593,45 +1685,6 @@ def run(args, wd):
     wd.cancel()
 
     if rank == 0:
-        total = B * world * args.steps
-        line = {
-            "metric": METRIC,
-            "value": total / dt,
-            "unit": "hands/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ramp": {"seconds": t_ramp, "steps": n_ramp, "step_ms": per_step * 1e3},
-            "kernel_events": {"every": every, "sampled_steps": len(sampled)},
-            "timed_region_rank0": region,
-            "ms_per_step": dt / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": args.precision,
-            "data": "synthetic (random-init MANO arrays of the official shapes, seed 0; "
-                    "Philox inputs keyed by (seed, global hand index): beta ~ N(0,1), "
-                    "pose ~ N(0,0.5^2) rad" + (", trans ~ U(-1,1) m" if with_trans else "") +
-                    ", generated on device)",
-            "config": {"workload": wl["desc"] if B == wl["hands"] else f"{args.workload} at {B} hands per GPU",
-                       "hands_per_gpu": B, "global_batch": B * world,
-                       "outputs": "verts+joints", "trans": with_trans, "path": args.path,
-                       "gather_to_gpu0": gather_on,
-                       "gather_impl": None if not gather_on else
-                       ({"sendrecv": "mano_gather (RCCL send/recv)", "allgather": "mano_allgather (RCCL ring)"}[impl]
-                        if gatherer is not None else "gloo rehearsal"),
-                       "parallelism": f"dp{world}"},
-            "process_group": ({"backend": args.backend, "world": world, "forced_at_one_rank": world == 1}
-                              if dist_on else None),
-            "roofline": roof,
-            "kernels": kernels,
-            "correctness": correctness,
-            "device_status": device_status,
-        }
-        if gather_info is not None:
-            line["gather"] = gather_info
-        if gather_check is not None:
-            line["gather_check"] = gather_check
         if legs is not None:
             line["legs"] = legs
         line.update(extra)

@@ -381,3 +381,30 @@ def test_bench_legs_one_rank_nccl():
     g = _check_legs(line["legs"], 1, {"C3": 131072, "C4": 65536})
     assert g["backend"] == "nccl" and g["comm_ranks"] == 1 and g["bytes_to_gpu0"] == 0
     assert g["compare"]["bit_exact"] and g["compare"]["ms"] > 0
+
+
+def test_bench_leg_hang_keeps_the_headline():
+    """A multi-GPU leg that hangs (rank 1 stalls at the start of C4) must not
+    cost the run its headline: the watchdog fires inside the leg, rank 0
+    prints the line with the measured value, the finished C3 leg and the
+    hung one named, and every rank exits 0 (the legs are not part of
+    `value`)."""
+    import json
+    import subprocess
+    import time
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                        "--batch", "2048", "--steps", "5", "--warmup", "1", "--ramp-seconds", "0",
+                        "--no-cpu", "--no-extra", "--no-dropin", "--no-live-pmc",
+                        "--leg-global", "C3=8192,C4=4096", "--leg-min-seconds", "5",
+                        "--inject-hang-leg", "1", "--watchdog-seconds", "45", "--pg-timeout-seconds", "200"],
+                       capture_output=True, text=True, timeout=170, env=env)
+    wall = time.monotonic() - t0
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["status"] == "ok" and line["value"] > 0 and line["correctness"]["pass"]
+    assert line["legs"]["C3"]["correctness"]["pass"]
+    assert line["legs"]["hung"]["phase"].startswith("leg_C4")
+    assert "C4" not in line["legs"]
+    assert wall < 150
