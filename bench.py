@@ -1269,6 +1269,11 @@ def run(args, wd):
                if gather_on and i % every == first else None for i in range(args.steps)]
     wd.enter("timed")
     t_open = time.perf_counter()
+    if dist_on and args.backend == "gloo":
+        # the rehearsal backend: ranks share one GPU, and gloo's barrier is
+        # host-only -- without this sync each rank would start its timed steps
+        # when its own queue drained, beside the others' ramps
+        torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize()   # the ramp and warmup end here: the GPU has not idled since the ramp began
