@@ -20,7 +20,7 @@
     defined(MANO_H3_BLOCKS) || defined(MANO_H3_DMA_PRIO) || defined(MANO_H3_FULL_WAIT) ||          \
     defined(MANO_H3_NO_PACK) || defined(MANO_H3_NT_STORE) || defined(MANO_H3_RING) || defined(MANO_H3_SPLIT_ACC) || defined(MANO_H3_SCALAR_UNSCALE) ||    \
     defined(MANO_H3_SKIN_PAIR) || defined(MANO_H3_TPW) || defined(MANO_H3_WAVES) ||                \
-    defined(MANO_PAIR_POLL_LIMIT) || defined(MANO_PAIR_ALIGN) || defined(MANO_PAIR_NT) || defined(MANO_PAIR_REVERSE) || defined(MANO_PAIR_INPLACE_FORWARD) || defined(MANO_PAIR_INPLACE_ORDER) || defined(MANO_PAIR_SLEEP_CMP) || defined(MANO_PAIR_SLEEP_MEM) || \
+    defined(MANO_PAIR_POLL_LIMIT) || defined(MANO_PAIR_ALIGN) || defined(MANO_PAIR_NT) || defined(MANO_PAIR_REVERSE) || defined(MANO_PAIR_INPLACE_FORWARD) || defined(MANO_PAIR_INPLACE_ORDER) || defined(MANO_PAIR_INPLACE_HOT) || defined(MANO_PAIR_SLEEP_CMP) || defined(MANO_PAIR_SLEEP_MEM) || \
     defined(MANO_PAIR_SLOTS) || defined(MANO_PAIR_STAMP) || defined(MANO_QUAD_ABLATE) ||           \
     defined(MANO_QUAD_GROUP_MAJOR) || defined(MANO_QUAD_MAX_GROUPS) || defined(MANO_QUAD_PAIR) ||  \
     defined(MANO_QUAD_PAIR_COMPUTE) || defined(MANO_QUAD_PAIR_PRIO) || defined(MANO_QUAD_P_EARLY) || \

@@ -621,12 +621,15 @@ struct PairStamp {
 #ifndef MANO_PAIR_INPLACE_ORDER
 #define MANO_PAIR_INPLACE_ORDER 0  // diagnostic builds: 1 = in-place units span-major, last span first
 #endif
+#ifndef MANO_PAIR_INPLACE_HOT
+#define MANO_PAIR_INPLACE_HOT 0  // in place: 1 = spans below hot_span0 read and written nontemporal
+#endif
 template <bool kTrans, bool kH3 = false, bool kAlign = false, bool kInPlace = false>
 __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     const float* __restrict__ transforms, const float* __restrict__ wfrag16,
     const float* __restrict__ vposed, const float* __restrict__ trans, float* __restrict__ verts,
     int64_t n, int n_verts, int n_groups, const uint16_t* __restrict__ basis_h3, float t_unscale,
-    int* __restrict__ status, const float* __restrict__ wfrag16v, int lp, unsigned shifts) {
+    int* __restrict__ status, const float* __restrict__ wfrag16v, int lp, unsigned shifts, int hot_span0) {
   static_assert(!(kAlign && kH3), "aligned units: fp32 only");
   static_assert(!(kInPlace && (kAlign || kH3)), "in-place units: fp32 plain units only");
   __shared__ f32x4 w_lds[kPairMaxGroups * 64];
@@ -792,6 +795,10 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     constexpr int kTrOps = (MANO_QUAD_ABLATE & 4) ? 0 : kQTrF4;
     constexpr int kDmaOps = kPairRowDmas + kTrOps + (kTrans ? 1 : 0);
     constexpr int kStoreOps = 3 + (kInPlace ? 2 : 0);  // per store call, on every path
+    // in place: spans below hot_span0 (full spans only; the launcher's
+    // estimate of what the blend GEMM left in the Infinity Cache) stream
+    // nontemporal, the hot ones with the default policy
+    constexpr bool kColdNt = kInPlace && MANO_PAIR_INPLACE_HOT;
     auto dma = [&](int64_t fq0, int fs0, int slot) {
       int64_t fq, h0;
       int fs, valid;
@@ -818,11 +825,21 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
         if (lane < 12)
           buffer_load_lds4(rr, lds_at(slot, unsigned(offsetof(PairStage, trans))), kAlign ? xo : 4 * lane, 0);
       }
+      if (kColdNt && __builtin_amdgcn_readfirstlane(fs) < hot_span0) {  // a uniform (scalar) branch
+        // a cold span (its v_posed left the Infinity Cache): read around it,
+        // so the stream does not push the hot spans' dirty lines out
 #pragma unroll
-      for (int r = 0; r < kQHands; ++r)
-        if (lane < row_f4)
-          buffer_load_lds16<kPairRowAux>(rv, lds_at(slot, unsigned(offsetof(PairStage, rows)) + 4u * r * kPStride),
-                                         kAlign && !full ? evo[r] : rvo[r], soff);
+        for (int r = 0; r < kQHands; ++r)
+          if (lane < row_f4)
+            buffer_load_lds16<2>(rv, lds_at(slot, unsigned(offsetof(PairStage, rows)) + 4u * r * kPStride), rvo[r],
+                                 soff);
+      } else {
+#pragma unroll
+        for (int r = 0; r < kQHands; ++r)
+          if (lane < row_f4)
+            buffer_load_lds16<kPairRowAux>(rv, lds_at(slot, unsigned(offsetof(PairStage, rows)) + 4u * r * kPStride),
+                                           kAlign && !full ? evo[r] : rvo[r], soff);
+      }
     };
     auto ds_read4 = [](unsigned addr) {
       return *reinterpret_cast<const __attribute__((address_space(3))) f32x4*>(uintptr_t(addr));
@@ -842,11 +859,17 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       f32x4 sdata[kQF4];
 #pragma unroll
       for (int i = 0; i < kQF4; ++i) sdata[i] = ds_read4((full ? fso[i] : tso[i]) + so);
+      if (kColdNt && __builtin_amdgcn_readfirstlane(fs) < hot_span0) {  // a uniform (scalar) branch
 #pragma unroll
-      for (int i = 0; i < kQF4; ++i)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sdata[i]), ro,
-                                               full ? fvo[i] : (kInPlace ? tvo_ip[i] : tvo[i]), soff,
-                                               kPairStoreAux);
+        for (int i = 0; i < kQF4; ++i)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sdata[i]), ro, fvo[i], soff, 2);
+      } else {
+#pragma unroll
+        for (int i = 0; i < kQF4; ++i)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sdata[i]), ro,
+                                                 full ? fvo[i] : (kInPlace ? tvo_ip[i] : tvo[i]), soff,
+                                                 kPairStoreAux);
+      }
       if constexpr (kInPlace) {
         // scalars first (a bit cast of a vector element reads element 0)
         const float e1 = sdata[0][1], e2 = sdata[0][2], e3 = sdata[0][3];
@@ -1097,10 +1120,22 @@ hipError_t launch_skin_quad(const DeviceModel& m, int64_t n, const float* transf
     if (h3 || !skin_in_place_supported(m, n)) return hipErrorNotSupported;
     const int64_t units = (n + kQHands - 1) / kQHands * (m.n_verts / kQVerts + (m.n_verts % kQVerts ? 1 : 0));
     const int64_t blocks_ip = std::min<int64_t>(units / (2 * kPairs), m.n_cu > 0 ? m.n_cu : 1);
+    // The spans the blend GEMM's v_posed most likely left dirty in the
+    // 256-MB Infinity Cache: blend_kernel's blocks walk the column tiles
+    // together, so when they all fit the chip at once (n / 128 blocks <= 2
+    // per CU) the last-written bytes are the LAST fraction of every row;
+    // spans wholly before it are cold.  (More blocks than that: the last
+    // hands are the hot ones, and the quads' last-first order serves them.)
+    constexpr double kMallBytes = 256.0 * 1024.0 * 1024.0;
+    const double row_bytes = double(n) * 3.0 * m.n_verts * 4.0;
+    const int64_t blend_blocks = (n + 127) / 128;
+    int hot_span0 = 0;
+    if (blend_blocks <= 2 * int64_t(m.n_cu > 0 ? m.n_cu : 1) && row_bytes > kMallBytes)
+      hot_span0 = int((1.0 - kMallBytes / row_bytes) * m.n_verts) / kQVerts;
     auto launch_ip = [&](auto kernel) {
       hipLaunchKernelGGL(kernel, dim3(unsigned(blocks_ip)), dim3(64 * kPairWaves), 0, stream, transforms,
                          m.wfrag16, vposed, trans, verts, n, m.n_verts, m.n_groups16, m.basis_h3,
-                         m.h3_lbs_unscale, m.status, nullptr, 0, 0u);
+                         m.h3_lbs_unscale, m.status, nullptr, 0, 0u, hot_span0);
     };
     if (trans) launch_ip(skin_pair_kernel<true, false, false, true>);
     else launch_ip(skin_pair_kernel<false, false, false, true>);
@@ -1145,7 +1180,7 @@ hipError_t launch_skin_quad(const DeviceModel& m, int64_t n, const float* transf
       auto launch_al = [&](auto kernel) {
         hipLaunchKernelGGL(kernel, dim3(unsigned(per_class * P)), dim3(64 * kPairWaves), 0, stream, transforms,
                            m.wfrag16, vposed, trans, verts, n, m.n_verts, m.n_groups16, m.basis_h3,
-                           m.h3_lbs_unscale, m.status, m.wfrag16v, lp, shifts);
+                           m.h3_lbs_unscale, m.status, m.wfrag16v, lp, shifts, 0);
       };
       if (trans) launch_al(skin_pair_kernel<true, false, true>);
       else launch_al(skin_pair_kernel<false, false, true>);
@@ -1155,7 +1190,7 @@ hipError_t launch_skin_quad(const DeviceModel& m, int64_t n, const float* transf
   auto launch = [&](auto kernel) {
     hipLaunchKernelGGL(kernel, dim3(unsigned(blocks)), dim3(64 * kPairWaves), 0, stream, transforms,
                        m.wfrag16, vposed, trans, verts, n, m.n_verts, m.n_groups16, m.basis_h3,
-                       m.h3_lbs_unscale, m.status, nullptr, 0, 0u);
+                       m.h3_lbs_unscale, m.status, nullptr, 0, 0u, 0);
   };
   if (h3) {
     if (trans) launch(skin_pair_kernel<true, true>);
