@@ -622,7 +622,7 @@ struct PairStamp {
 #define MANO_PAIR_INPLACE_ORDER 0  // diagnostic builds: 1 = in-place units span-major, last span first
 #endif
 #ifndef MANO_PAIR_INPLACE_HOT
-#define MANO_PAIR_INPLACE_HOT 0  // in place: 1 = spans below hot_span0 read and written nontemporal
+#define MANO_PAIR_INPLACE_HOT 0  // in place, spans below hot_span0: bit 0 = read nontemporal, bit 1 = written nontemporal
 #endif
 template <bool kTrans, bool kH3 = false, bool kAlign = false, bool kInPlace = false>
 __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
@@ -798,7 +798,8 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
     // in place: spans below hot_span0 (full spans only; the launcher's
     // estimate of what the blend GEMM left in the Infinity Cache) stream
     // nontemporal, the hot ones with the default policy
-    constexpr bool kColdNt = kInPlace && MANO_PAIR_INPLACE_HOT;
+    constexpr bool kColdNtRead = kInPlace && (MANO_PAIR_INPLACE_HOT & 1);
+    constexpr bool kColdNtStore = kInPlace && (MANO_PAIR_INPLACE_HOT & 2);
     auto dma = [&](int64_t fq0, int fs0, int slot) {
       int64_t fq, h0;
       int fs, valid;
@@ -825,7 +826,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
         if (lane < 12)
           buffer_load_lds4(rr, lds_at(slot, unsigned(offsetof(PairStage, trans))), kAlign ? xo : 4 * lane, 0);
       }
-      if (kColdNt && __builtin_amdgcn_readfirstlane(fs) < hot_span0) {  // a uniform (scalar) branch
+      if (kColdNtRead && __builtin_amdgcn_readfirstlane(fs) < hot_span0) {  // a uniform (scalar) branch
         // a cold span (its v_posed left the Infinity Cache): read around it,
         // so the stream does not push the hot spans' dirty lines out
 #pragma unroll
@@ -859,7 +860,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(
       f32x4 sdata[kQF4];
 #pragma unroll
       for (int i = 0; i < kQF4; ++i) sdata[i] = ds_read4((full ? fso[i] : tso[i]) + so);
-      if (kColdNt && __builtin_amdgcn_readfirstlane(fs) < hot_span0) {  // a uniform (scalar) branch
+      if (kColdNtStore && __builtin_amdgcn_readfirstlane(fs) < hot_span0) {  // a uniform (scalar) branch
 #pragma unroll
         for (int i = 0; i < kQF4; ++i)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sdata[i]), ro, fvo[i], soff, 2);
