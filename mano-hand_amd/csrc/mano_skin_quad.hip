@@ -606,10 +606,14 @@ struct PairStamp {
 // extra stores (dropped: an offset past num_records), so the step's
 // vector-memory op count stays fixed.  The tail's reads of the d shared
 // vertices may then see the span's skinned values; they feed only the d
-// outputs it does not store.  Hand quads go last-first: the blend GEMM's last
-// ~256 MB of v_posed are still dirty in the Infinity Cache when the LBS
-// starts, so their reads hit and their lines are overwritten in the cache
-// instead of being written back first.  (In place,
+// outputs it does not store.  The blend GEMM's last ~256 MB of v_posed are
+// still dirty in the Infinity Cache when the LBS starts -- with all its
+// blocks resident at once (n <= 65,536), the last ~42 % of EVERY row -- so
+// the LBS reads those lines as hits and overwrites them in the cache instead
+// of having them written back first, provided the rest of its stream does
+// not evict them: the cold spans go nontemporal (MANO_PAIR_INPLACE_HOT
+// below).  Hand quads go last-first (for larger batches the hot lines are the
+// last hands' rows).  (In place,
 // `vposed` and `verts` alias despite their __restrict__: the kernel touches
 // both only through buffer intrinsics on resource descriptors -- the rows'
 // LDS-DMA and the memory wave's stores, ordered by its counted vmcnt -- never
@@ -621,8 +625,15 @@ struct PairStamp {
 #ifndef MANO_PAIR_INPLACE_ORDER
 #define MANO_PAIR_INPLACE_ORDER 0  // diagnostic builds: 1 = in-place units span-major, last span first
 #endif
+// In place, the spans the launcher estimates cold (below hot_span0: their
+// v_posed already left the Infinity Cache) are read AND written nontemporal,
+// so streaming them does not push out the hot spans' dirty lines before the
+// LBS overwrites them: 0.2555-0.2581 vs 0.2717-0.2727 ms in the unfused path
+// (62 vs 58.6 % of 8 TB/s), bit-identical; either bit alone gains nothing
+// (stores only 0.271) or loses (reads only 0.285), profiles/r06/r06q_*,
+// r06r_*.  (Diagnostic builds: bit 0 = reads, bit 1 = stores.)
 #ifndef MANO_PAIR_INPLACE_HOT
-#define MANO_PAIR_INPLACE_HOT 0  // in place, spans below hot_span0: bit 0 = read nontemporal, bit 1 = written nontemporal
+#define MANO_PAIR_INPLACE_HOT 3
 #endif
 template <bool kTrans, bool kH3 = false, bool kAlign = false, bool kInPlace = false>
 __global__ __launch_bounds__(64 * kPairWaves, 1) void skin_pair_kernel(

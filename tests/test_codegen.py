@@ -153,3 +153,46 @@ def test_product_build_sets_no_diagnostic_switch():
     assert run("-DMANO_BS_ABLATE=1", "-DMANO_DIAGNOSTIC_BUILD=1").returncode == 0
     with pytest.raises(ValueError):
         g.build_library(g.LIB, ["-DMANO_BS_ABLATE=1"])
+
+
+def _prog_insts(lines):
+    """(addr, mnemonic, operands, branch target) tuples, 4 bytes apart; a
+    target is given as the index of the instruction it jumps to."""
+    out = []
+    for k, (mn, ops, tgt) in enumerate(lines):
+        out.append((4 * k, mn, ops, None if tgt is None else 4 * tgt))
+    return out
+
+
+def test_vmcnt_scan_follows_the_structurizer_flow_variable():
+    """tools/isa_scan.py on the shape the compiler gives a uniform if / else
+    (skin_pair's in-place cold / hot spans): arm A guarded by an SCC branch
+    clears a flow variable, arm B is skipped through `s_andn2_b64 vcc, exec,
+    flow` -- every followed path runs exactly one arm, so the 2-op DMA group
+    checks out.  Without the flow variable (a genuine both-arms path) the
+    same program fails."""
+    isa_scan = _tools()
+    dma, st = ("buffer_load_dwordx4", "v1, s[0:3], 0 offen lds", None), ("buffer_store_dwordx4", "v[0:3], v4, s[0:3], 0 offen", None)
+    body = [
+        dma, dma,                                   # 0-1: unit k's DMA group (2 ops)
+        st, st, st,                                 # 2-4: stores
+        ("s_mov_b64", "s[44:45], -1", None),        # 5: flow = -1
+        ("s_cbranch_scc1", "1", 9),                 # 6: cold -> skip arm A
+        dma, dma,                                   # 7-8: arm A (default policy)
+        ("s_mov_b64", "s[44:45], 0", None),         # 9: (A ran) flow = 0   [target of 6 is 10 below]
+        ("s_andn2_b64", "vcc, exec, s[44:45]", None),
+        ("s_cbranch_vccnz", "1", 14),               # 11: A ran -> skip arm B
+        ("buffer_load_dwordx4", "v1, s[0:3], 0 offen nt lds", None),
+        ("buffer_load_dwordx4", "v1, s[0:3], 0 offen nt lds", None),
+        ("s_waitcnt", "vmcnt(5)", None),            # 14
+        ("s_endpgm", "", None),
+    ]
+    body[6] = ("s_cbranch_scc1", "1", 10)
+    n, fails = isa_scan.check_vmcnt_protocol(_prog_insts(body), 2, 5, n_stores=3)
+    assert n == 1 and fails == [], fails
+    broken = [l for k, l in enumerate(body) if k not in (5, 9)]   # no flow variable: vcc unknown
+    for k, l in enumerate(broken):
+        if l[0].startswith("s_cbranch") and l[2] is not None:
+            broken[k] = (l[0], l[1], l[2] - (1 if l[2] > 5 else 0) - (1 if l[2] > 9 else 0))
+    n, fails = isa_scan.check_vmcnt_protocol(_prog_insts(broken), 2, 5, n_stores=3)
+    assert n == 1 and fails, "a path through both arms must fail"

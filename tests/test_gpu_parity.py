@@ -456,13 +456,16 @@ def test_standalone_lbs_ragged(engine, dev, params, B, with_trans):
 
 
 @pytest.mark.parametrize("B,with_trans", [(1, True), (2, False), (3, True), (5, False), (1023, True),
+                                         (40000, True), (65533, False), (65536, True),
                                          (65537, True), (65538, False)])
 def test_standalone_lbs_in_place(engine, dev, params, B, with_trans):
     """The LBS in place (mano_stage_skin with rest_verts == verts, ABI 7: the
     blend GEMM writes v_posed into verts, skin_pair's in-place units
     overwrite it -- the tail unit stores only its own 10 vertices, hand
-    quads last-first) == the fused kernel's verts bit for bit, ragged
-    batches included; the rows past the batch stay untouched."""
+    quads last-first; at 40,000-65,536 hands the spans the launcher deems
+    cold -- 0-2 and 0-6 -- stream nontemporal) == the fused kernel's verts
+    bit for bit, ragged batches included; the rows past the batch stay
+    untouched."""
     rng = np.random.default_rng(700 + B)
     betas = f32(rng.normal(0, 1, (B, 10)), dev)
     pose = f32(rng.normal(0, 0.6, (B, 16, 3)), dev)

@@ -35,6 +35,7 @@ for s in ${STEPS:-tests bench}; do
     inplace_span) step inplace_span 400 python tools/debug/time_inplace.py libmano_hip.so libmano_hip_ipspan.so --reps 3 ;;
     inplace_hot) step inplace_hot 500 python tools/debug/time_inplace.py libmano_hip.so libmano_hip_iphot.so --reps 3 ;;
     inplace_hot2) step inplace_hot2 600 python tools/debug/time_inplace.py libmano_hip.so libmano_hip_iphot.so libmano_hip_iphots.so libmano_hip_iphotr.so --reps 2 ;;
+    inplace_final) step inplace_final 500 python tools/debug/time_inplace.py libmano_hip.so libmano_hip_iphot0.so --reps 3 ;;
     inplace_nt) step inplace_nt 500 python tools/debug/time_inplace.py libmano_hip.so libmano_hip_ipnt1.so libmano_hip_ipnt2.so libmano_hip_ipnt3.so --reps 2 ;;
     # the driver's N = 8 command with the multi-GPU legs (C3 2^24 and C4 2^22
     # at their BASELINE sizes), 8 gloo ranks sharing this box's GPU

@@ -112,19 +112,49 @@ def _vmem_kind(mn, ops):
     return None
 
 
+_SREG = r"s\[\d+:\d+\]"
+
+
+def _flow_step(mn, ops, consts, vcc):
+    """The structurizer's flow variables, tracked along a path: an SGPR pair
+    set to a constant (s_mov_b64 s[a:b], -1 / 0) and `s_andn2_b64 vcc, exec,
+    s[a:b]` of a known pair (vcc nonzero iff the pair is 0 -- exec is never 0
+    here: every exec-masked region of the memory wave keeps lane 0).  An
+    if / else whose arms the compiler emitted as two guarded blocks (the
+    second skipped through such a vcc) then has exactly one arm on every
+    path the scan follows.  Any other write to a tracked register forgets
+    it.  Returns (consts, vcc) after the instruction; vcc is True / False /
+    None (unknown)."""
+    parts = [p.strip() for p in ops.split(",")] if ops else []
+    dst = parts[0] if parts else ""
+    m = re.fullmatch(_SREG, dst) if mn == "s_mov_b64" else None
+    if m and len(parts) > 1 and parts[1] in ("-1", "0"):
+        return dict(consts, **{dst: int(parts[1])}), (None if dst == "vcc" else vcc)
+    if mn == "s_andn2_b64" and dst == "vcc" and len(parts) == 3 and parts[1] == "exec" and parts[2] in consts:
+        return consts, consts[parts[2]] == 0
+    if dst in consts:
+        consts = {k: v for k, v in consts.items() if k != dst}
+    if dst == "vcc" or dst.startswith("vcc"):
+        vcc = None
+    return consts, vcc
+
+
 def check_vmcnt_protocol(insts, n_dma, n_wait, n_stores=N_STORES):
     """Every path from the function entry to each `s_waitcnt vmcnt(n_wait)`
     must end with [dma]+ [other]{>=n_stores} [dma]{n_dma} (see the module
-    docstring).  Returns (n_waits_found, [failure strings])."""
+    docstring).  Paths that the structurizer's flow variables rule out
+    (`_flow_step`) are not followed.  Returns (n_waits_found, [failure
+    strings])."""
     idx = {a: i for i, (a, _, _, _) in enumerate(insts)}
     waits = {i for i, (_, mn, ops, _) in enumerate(insts)
              if mn == "s_waitcnt" and re.search(rf"\bvmcnt\({n_wait}\)", ops)}
     keep = n_dma + n_stores + 8
-    failures, seen, stack = [], set(), [(0, ())]
+    failures, seen, stack = [], set(), [(0, (), (), None)]
     while stack:
-        i, tail = stack.pop()
+        i, tail, cst, vcc = stack.pop()
+        consts = dict(cst)
         while i < len(insts):
-            state = (i, tail)
+            state = (i, tail, tuple(sorted(consts.items())), vcc)
             if state in seen:
                 break
             seen.add(state)
@@ -153,11 +183,21 @@ def check_vmcnt_protocol(insts, n_dma, n_wait, n_stores=N_STORES):
                     break
                 i = idx[tgt]
                 continue
+            if mn in ("s_cbranch_vccnz", "s_cbranch_vccz") and vcc is not None:
+                if tgt is None or tgt not in idx:
+                    failures.append(f"unresolved branch at 0x{a:x}")
+                    break
+                if vcc == (mn == "s_cbranch_vccnz"):   # taken: the only feasible successor
+                    i = idx[tgt]
+                    continue
+                i += 1
+                continue
             if mn.startswith("s_cbranch") and mn != "s_cbranch_execz":
                 if tgt is None or tgt not in idx:
                     failures.append(f"unresolved branch at 0x{a:x}")
                     break
-                stack.append((idx[tgt], tail))
+                stack.append((idx[tgt], tail, tuple(sorted(consts.items())), vcc))
+            consts, vcc = _flow_step(mn, ops, consts, vcc)
             i += 1
     return len(waits), failures
 
