@@ -132,11 +132,25 @@ def _flow_step(mn, ops, consts, vcc):
         return dict(consts, **{dst: int(parts[1])}), (None if dst == "vcc" else vcc)
     if mn == "s_andn2_b64" and dst == "vcc" and len(parts) == 3 and parts[1] == "exec" and parts[2] in consts:
         return consts, consts[parts[2]] == 0
-    if dst in consts:
-        consts = {k: v for k, v in consts.items() if k != dst}
+    # any write that touches a tracked pair (the pair itself, one of its
+    # halves or a wider range) forgets it
+    written = _sgprs(dst)
+    if written:
+        consts = {k: v for k, v in consts.items() if not (_sgprs(k) & written)}
     if dst == "vcc" or dst.startswith("vcc"):
         vcc = None
     return consts, vcc
+
+
+def _sgprs(op):
+    """The SGPR numbers an operand names (s7 -> {7}, s[44:45] -> {44, 45})."""
+    m = re.fullmatch(r"s(\d+)", op)
+    if m:
+        return {int(m.group(1))}
+    m = re.fullmatch(r"s\[(\d+):(\d+)\]", op)
+    if m:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    return set()
 
 
 def check_vmcnt_protocol(insts, n_dma, n_wait, n_stores=N_STORES):
