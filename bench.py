@@ -26,7 +26,11 @@ the hot path).
 Before the untimed warmup the bench runs the step for `--ramp-seconds`
 (reported as `ramp`): the chip needs ~50 back-to-back launches to reach its
 steady clock (profiles/r01_kernel_trace_warmup.txt), so a short `--warmup`
-does not leave the timed steps on the ramp.
+does not leave the timed steps on the ramp; the ramp's length is fixed up
+front (agreed by the ranks), and the ramp, the warmup and the opening
+barrier run with no idle GPU in between.  `timed_region_rank0` splits the
+timed region's host time (issue, sync, closing barrier) and gives the GPU
+time per step.
 
 Rank 0 prints ONE JSON line with the whole-node hands/s, the roofline of the
 dominant kernel (per-kernel durations from HIP events recorded on the launch
@@ -36,6 +40,13 @@ by two rocprofv3 --pmc passes, FETCH_SIZE and WRITE_SIZE, over a short child
 run of this bench on rank 0's GPU after the timed region) and the CPU baseline:
 the float64 restatement of mano_np.py (oracle/, "port") timed on this host's
 cores by rank 0 at every N (the other ranks wait with idle GPUs).
+
+Every N > 1 run then measures BASELINE's multi-GPU configs as legs, after
+the headline and not part of `value` (`legs` in the line; --legs auto|on|off):
+C3 = 2^24 hands strong-scaled over the ranks, C4 = 2^22 hands + the gather of
+verts + joints to GPU 0 (RCCL mano_gather; the ring all-gather beside it),
+each with its own oracle / bit-exact checks.  A failing leg is recorded; a
+hung one ends in the watchdog's line, which keeps the headline.
 
 Failure handling with a process group (every N > 1 run): a collective that
 stalls raises after --pg-timeout-seconds (240); a rank still inside the
