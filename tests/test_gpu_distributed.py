@@ -96,7 +96,7 @@ def test_bench_c4_gather_rehearsal_layout(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(world), "--backend", "gloo",
                         "--workload", "C4", "--batch", str(B), "--steps", "5", "--warmup", "1",
                         "--ramp-seconds", "0", "--cpu-seconds", "1", "--cpu-procs", "2", "--no-extra",
-                        "--no-dropin", "--dump-gather", str(dump)],
+                        "--no-dropin", "--dump-gather", str(dump), "--legs", "off"],
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
@@ -280,7 +280,7 @@ def test_bench_c4_ramp_ends_together():
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo",
                         "--workload", "C4", "--batch", "256", "--steps", "5", "--warmup", "2",
                         "--ramp-seconds", "1", "--no-cpu", "--no-extra", "--no-dropin", "--no-live-pmc",
-                        "--watchdog-seconds", "200"],
+                        "--watchdog-seconds", "200", "--legs", "off"],
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
@@ -302,7 +302,8 @@ def test_bench_watchdog_in_a_gpu_run():
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo",
                         "--batch", "1024", "--steps", "5", "--warmup", "1", "--ramp-seconds", "0.2",
                         "--no-cpu", "--no-extra", "--no-dropin", "--no-live-pmc",
-                        "--inject-hang", "1", "--watchdog-seconds", "30", "--pg-timeout-seconds", "200"],
+                        "--inject-hang", "1", "--watchdog-seconds", "30", "--pg-timeout-seconds", "200",
+                        "--legs", "off"],
                        capture_output=True, text=True, timeout=170, env=env)
     wall = time.monotonic() - t0
     assert r.returncode != 0
